@@ -1,0 +1,49 @@
+# Build of the MI355X-native library + CLIs (gfx950 only). `make -j8`.
+#   deepreadmapper_amd/libdrm_hip.so : C ABI (include/drm_hip.h), HIP kernels + host C++
+#   bin/pipeline, bin/hnswpq_index   : drop-in CLIs for src/main.cpp and src/hnswpq/index.cpp
+#   oracle/*.so                      : TEST-ONLY checker (oracle/Makefile)
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+ARCH ?= gfx950
+CXX ?= g++
+BUILD := build
+PKG := deepreadmapper_amd
+SRC := $(PKG)/csrc
+
+COMMON := -O3 -std=c++17 -fPIC -Iinclude -I$(SRC) -Wall -Wno-unused-result
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -ffp-contract=off -munsafe-fp-atomics
+HOSTFLAGS := $(COMMON) -fopenmp -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+
+LIB := $(PKG)/libdrm_hip.so
+HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/sw_rerank.o $(BUILD)/capi.o
+HOST_OBJS := $(BUILD)/faiss_io.o $(BUILD)/formats.o $(BUILD)/builder.o $(BUILD)/embed.o
+HDRS := include/drm_hip.h $(SRC)/drm_internal.h $(SRC)/drm_device.h
+
+all: $(LIB) bin/pipeline bin/hnswpq_index oracle
+
+$(BUILD):
+	mkdir -p $(BUILD) bin
+
+$(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/capi.o: $(SRC)/capi.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(HOST_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lgomp -Wl,-soname,libdrm_hip.so
+
+bin/%: tools/%.cpp $(LIB) $(HDRS) | $(BUILD)
+	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -ldrm_hip -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(PKG)' -Wl,-rpath,$(ROCM)/lib
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) bin $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

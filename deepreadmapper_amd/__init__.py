@@ -1,0 +1,9 @@
+"""deepreadmapper_amd -- MI355X-native drop-in for DeepReadMapper's query hot path:
+HNSW-PQ candidate search (faiss_search) + Smith-Waterman rerank (post_process_sw_static),
+implemented as HIP kernels for gfx950 behind the C ABI in include/drm_hip.h."""
+from ._native import DrmError, lib  # noqa: F401  (ImportError if libdrm_hip.so is missing)
+from .search import HnswPqIndex, faiss_search, read_index  # noqa: F401
+from .rerank import (WindowTable, calc_sw_score, calc_sw_scores, post_process_sw_static,  # noqa: F401
+                     rerank_arrays, sw_reranker)
+
+__version__ = "0.1.0"

@@ -1,0 +1,118 @@
+"""ctypes binding of libdrm_hip.so (include/drm_hip.h).
+
+The library is built in-tree (`make` / `__graft_entry__.build()`). Importing this module without it
+raises ImportError: there is no CPU fallback on the product path.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdrm_hip.so")
+
+DRM_OK = 0
+DRM_ERR_ARG = -1
+DRM_ERR_IO = -2
+DRM_ERR_FORMAT = -3
+DRM_ERR_HIP = -4
+DRM_ERR_CANDS = -5
+DRM_ERR_K = -6
+DRM_ERR_UNSUPPORTED = -7
+
+# Every symbol include/drm_hip.h declares (checked by tests/test_capi_exports.py).
+EXPORTS = [
+    "drm_last_error", "drm_version", "drm_device_count", "drm_set_device", "drm_device_sync", "drm_malloc",
+    "drm_free", "drm_memset", "drm_memcpy_h2d", "drm_memcpy_d2h", "drm_stream_create", "drm_stream_destroy",
+    "drm_stream_sync", "drm_event_create", "drm_event_destroy", "drm_event_record", "drm_event_elapsed_ms",
+    "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device", "drm_sw_scores",
+    "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
+    "drm_build_hnswpq", "drm_embed_kmer3",
+]
+
+
+class DrmError(RuntimeError):
+    """Raised for a non-zero return code; `.code` is the DRM_ERR_* value."""
+
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("d", C.c_int32), ("ntotal", C.c_int64), ("pq_M", C.c_int32), ("pq_nbits", C.c_int32),
+                ("M_hnsw", C.c_int32), ("max_level", C.c_int32), ("entry_point", C.c_int32),
+                ("efConstruction", C.c_int32), ("efSearch", C.c_int32), ("metric_type", C.c_int32),
+                ("device_bytes", C.c_int64)]
+
+
+class SearchStats(C.Structure):
+    _fields_ = [("nq", C.c_int64), ("ndis", C.c_int64), ("nhops", C.c_int64), ("kernel_ms", C.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+                          "deepreadmapper_amd has no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
+    sigs = {
+        "drm_last_error": (C.c_char_p, []),
+        "drm_version": (C.c_int, []),
+        "drm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "drm_set_device": (C.c_int, [C.c_int]),
+        "drm_device_sync": (C.c_int, []),
+        "drm_malloc": (C.c_int, [C.POINTER(vp), sz]),
+        "drm_free": (C.c_int, [vp]),
+        "drm_memset": (C.c_int, [vp, C.c_int, sz]),
+        "drm_memcpy_h2d": (C.c_int, [vp, vp, sz]),
+        "drm_memcpy_d2h": (C.c_int, [vp, vp, sz]),
+        "drm_stream_create": (C.c_int, [C.POINTER(vp)]),
+        "drm_stream_destroy": (C.c_int, [vp]),
+        "drm_stream_sync": (C.c_int, [vp]),
+        "drm_event_create": (C.c_int, [C.POINTER(vp)]),
+        "drm_event_destroy": (C.c_int, [vp]),
+        "drm_event_record": (C.c_int, [vp, vp]),
+        "drm_event_elapsed_ms": (C.c_int, [vp, vp, C.POINTER(C.c_float)]),
+        "drm_index_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
+        "drm_index_free": (C.c_int, [vp]),
+        "drm_index_get_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
+        "drm_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
+        "drm_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
+        "drm_sw_scores": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp]),
+        "drm_refs_create": (C.c_int, [vp, i64, i32, i64, C.c_int, C.POINTER(vp)]),
+        "drm_refs_free": (C.c_int, [vp]),
+        "drm_post_process_sw_static": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
+                                                 C.POINTER(i64)]),
+        "drm_post_process_sw_static_device": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
+                                                        vp]),
+        "drm_build_hnswpq": (C.c_int, [vp, i64, i32, i32, i32, i32, i32, C.c_double, i32, C.c_uint64,
+                                       C.c_char_p]),
+        "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != DRM_OK:
+        msg = lib().drm_last_error()
+        raise DrmError(rc, msg.decode() if msg else f"error {rc}")
+    return rc
+
+
+def ptr(a):
+    """Host pointer of a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return a.ctypes.data

@@ -1,0 +1,538 @@
+// deepreadmapper_amd/csrc/capi.cpp -- implementation of include/drm_hip.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <unordered_set>
+
+#include "drm_device.h"
+
+namespace drm {
+static thread_local std::string g_last_error;
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+} // namespace drm
+
+struct drm_index {
+    drm::DeviceIndex dev;
+};
+struct drm_refs {
+    drm::DeviceRefs dev;
+};
+
+using drm::Error;
+
+template <class F> static int guarded(F &&f)
+{
+    try {
+        f();
+        return DRM_OK;
+    } catch (const Error &e) {
+        drm::set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        drm::set_last_error("out of host memory");
+        return DRM_ERR_ARG;
+    } catch (const std::exception &e) {
+        drm::set_last_error(e.what());
+        return DRM_ERR_ARG;
+    }
+}
+
+namespace {
+template <class T> struct DevBuf { // RAII device buffer for host-pointer entry points
+    T *p = nullptr;
+    size_t n = 0;
+    explicit DevBuf(size_t count) : n(count)
+    {
+        if (count)
+            DRM_HIP_CHECK(hipMalloc(&p, sizeof(T) * count));
+    }
+    ~DevBuf()
+    {
+        if (p)
+            (void)hipFree(p);
+    }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    void upload(const T *h) { DRM_HIP_CHECK(hipMemcpy(p, h, sizeof(T) * n, hipMemcpyHostToDevice)); }
+    void download(T *h) const { DRM_HIP_CHECK(hipMemcpy(h, p, sizeof(T) * n, hipMemcpyDeviceToHost)); }
+};
+
+template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
+{
+    T *p = nullptr;
+    size_t nb = sizeof(T) * std::max<size_t>(v.size(), 1);
+    DRM_HIP_CHECK(hipMalloc(&p, nb));
+    if (!v.empty())
+        DRM_HIP_CHECK(hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    bytes += (int64_t)nb;
+    return p;
+}
+
+void free_index(drm::DeviceIndex &d)
+{
+    void *ptrs[] = {d.centroids, d.codes, d.nbr0, d.upper_off, d.upper_nbr, d.visited, d.clear_list, d.counter};
+    for (void *p : ptrs)
+        if (p)
+            (void)hipFree(p);
+}
+} // namespace
+
+extern "C" {
+
+const char *drm_last_error(void) { return drm::g_last_error.c_str(); }
+int drm_version(void) { return 100; /* 0.1.0 */ }
+
+int drm_device_count(int *n)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipGetDeviceCount(n)); });
+}
+int drm_set_device(int device)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipSetDevice(device)); });
+}
+int drm_device_sync(void)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipDeviceSynchronize()); });
+}
+int drm_malloc(void **ptr, size_t bytes)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipMalloc(ptr, std::max<size_t>(bytes, 1))); });
+}
+int drm_free(void *ptr)
+{
+    return guarded([&] {
+        if (ptr)
+            DRM_HIP_CHECK(hipFree(ptr));
+    });
+}
+int drm_memset(void *ptr, int value, size_t bytes)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipMemset(ptr, value, bytes)); });
+}
+int drm_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)); });
+}
+int drm_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)); });
+}
+int drm_stream_create(void **stream)
+{
+    return guarded([&] {
+        hipStream_t s;
+        DRM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *stream = (void *)s;
+    });
+}
+int drm_stream_destroy(void *stream)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipStreamDestroy((hipStream_t)stream)); });
+}
+int drm_stream_sync(void *stream)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream)); });
+}
+int drm_event_create(void **ev)
+{
+    return guarded([&] {
+        hipEvent_t e;
+        DRM_HIP_CHECK(hipEventCreate(&e));
+        *ev = (void *)e;
+    });
+}
+int drm_event_destroy(void *ev)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipEventDestroy((hipEvent_t)ev)); });
+}
+int drm_event_record(void *ev, void *stream)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream)); });
+}
+int drm_event_elapsed_ms(void *start, void *stop, float *ms)
+{
+    return guarded([&] {
+        DRM_HIP_CHECK(hipEventSynchronize((hipEvent_t)stop));
+        DRM_HIP_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    });
+}
+
+// ------------------------------------------------------------------------------------ index
+int drm_index_load(const char *path, int device, drm_index **out)
+{
+    return guarded([&] {
+        if (!path || !out)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *out = nullptr;
+        drm::HnswPqHost h = drm::read_hnswpq(path);
+        if ((int)h.cum_nneighbor_per_level.size() - 1 > drm::kMaxLevels)
+            throw Error(DRM_ERR_UNSUPPORTED, "more than 24 HNSW levels");
+        DRM_HIP_CHECK(hipSetDevice(device));
+        std::unique_ptr<drm_index> ix(new drm_index());
+        drm::DeviceIndex &d = ix->dev;
+        d.device = device;
+        d.d = h.hdr.d;
+        d.ntotal = h.hdr.ntotal;
+        d.pq_M = (int)h.pq_M;
+        d.pq_nbits = (int)h.pq_nbits;
+        d.dsub = h.dsub();
+        d.ksub = h.ksub();
+        d.code_size = h.code_size();
+        d.deg0 = h.deg0();
+        d.n_levels = (int)h.cum_nneighbor_per_level.size() - 1;
+        d.max_level = h.max_level;
+        d.entry_point = h.entry_point;
+        for (size_t l = 0; l < h.cum_nneighbor_per_level.size(); ++l)
+            d.cum[l] = h.cum_nneighbor_per_level[l];
+        // level-0 rows, dense [ntotal][deg0]
+        const int64_t n = h.hdr.ntotal;
+        std::vector<int32_t> nbr0((size_t)n * d.deg0);
+        std::vector<uint32_t> upper_off((size_t)n, ~0u);
+        std::vector<int32_t> upper;
+        for (int64_t i = 0; i < n; ++i) {
+            const uint64_t o = h.offsets[(size_t)i];
+            std::memcpy(&nbr0[(size_t)i * d.deg0], &h.neighbors[o + h.cum_nneighbor_per_level[0]],
+                        sizeof(int32_t) * d.deg0);
+            const int lv = h.levels[(size_t)i];
+            if (lv > 1) {
+                if (upper.size() > 0xF0000000ull)
+                    throw Error(DRM_ERR_UNSUPPORTED, "upper-level link table exceeds 32-bit offsets");
+                upper_off[(size_t)i] = (uint32_t)upper.size();
+                upper.insert(upper.end(), h.neighbors.begin() + (o + h.cum_nneighbor_per_level[1]),
+                             h.neighbors.begin() + (o + h.cum_nneighbor_per_level[lv]));
+            }
+            // a row listing one id twice changes visited-set semantics: flag it for the kernel
+            if (!d.has_dup_links) {
+                const int32_t *r = &nbr0[(size_t)i * d.deg0];
+                for (int a = 0; a < d.deg0 && r[a] >= 0 && !d.has_dup_links; ++a)
+                    for (int b = a + 1; b < d.deg0 && r[b] >= 0; ++b)
+                        if (r[a] == r[b]) {
+                            d.has_dup_links = 1;
+                            break;
+                        }
+            }
+        }
+        d.upper_len = (int64_t)upper.size();
+        try {
+            d.centroids = upload_vec(h.centroids, d.device_bytes);
+            d.codes = upload_vec(h.codes, d.device_bytes);
+            d.nbr0 = upload_vec(nbr0, d.device_bytes);
+            d.upper_off = upload_vec(upper_off, d.device_bytes);
+            d.upper_nbr = upload_vec(upper, d.device_bytes);
+        } catch (...) {
+            free_index(d);
+            throw;
+        }
+        // keep header metadata only
+        d.meta.hdr = h.hdr;
+        d.meta.efConstruction = h.efConstruction;
+        d.meta.efSearch = h.efSearch;
+        d.meta.entry_point = h.entry_point;
+        d.meta.max_level = h.max_level;
+        d.meta.pq_M = h.pq_M;
+        d.meta.pq_nbits = h.pq_nbits;
+        d.meta.cum_nneighbor_per_level = h.cum_nneighbor_per_level;
+        *out = ix.release();
+    });
+}
+
+int drm_index_free(drm_index *index)
+{
+    return guarded([&] {
+        if (!index)
+            return;
+        (void)hipSetDevice(index->dev.device);
+        free_index(index->dev);
+        delete index;
+    });
+}
+
+int drm_index_get_info(const drm_index *index, drm_index_info *info)
+{
+    return guarded([&] {
+        if (!index || !info)
+            throw Error(DRM_ERR_ARG, "null argument");
+        const drm::DeviceIndex &d = index->dev;
+        info->d = d.d;
+        info->ntotal = d.ntotal;
+        info->pq_M = d.pq_M;
+        info->pq_nbits = d.pq_nbits;
+        info->M_hnsw = d.deg0 / 2;
+        info->max_level = d.max_level;
+        info->entry_point = d.entry_point;
+        info->efConstruction = d.meta.efConstruction;
+        info->efSearch = d.meta.efSearch;
+        info->metric_type = d.meta.hdr.metric_type;
+        info->device_bytes = d.device_bytes;
+    });
+}
+
+int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                      int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, void *stream)
+{
+    return guarded([&] {
+        if (!index)
+            throw Error(DRM_ERR_ARG, "null index");
+        if (n <= 0)
+            throw Error(DRM_ERR_ARG, "Query data is empty");
+        if (n >= (int64_t)1 << 31)
+            throw Error(DRM_ERR_ARG, "more than 2^31-1 queries in one call");
+        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
+        int32_t *nd = d_ndis, *nh = d_nhops;
+        std::unique_ptr<DevBuf<int32_t>> tmp;
+        if (!nd || !nh) {
+            tmp.reset(new DevBuf<int32_t>((size_t)n * 2));
+            if (!nd)
+                nd = tmp->p;
+            if (!nh)
+                nh = tmp->p + n;
+        }
+        drm::launch_hnsw_search(index->dev, d_x, n, k, ef, d_D, d_I, nd, nh, (hipStream_t)stream);
+        if (tmp)
+            DRM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    });
+}
+
+int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k, int32_t ef, float *D, int64_t *I,
+               drm_search_stats *stats)
+{
+    return guarded([&] {
+        if (!index || !x || !D || !I)
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (n <= 0)
+            throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswpq/search.cpp:16-19
+        if (d != index->dev.d)
+            throw Error(DRM_ERR_ARG, "query dimension " + std::to_string(d) + " != index dimension " +
+                                         std::to_string(index->dev.d));
+        if (k <= 0)
+            throw Error(DRM_ERR_ARG, "k must be > 0");
+        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
+        DevBuf<float> dx((size_t)n * d), dD((size_t)n * k);
+        DevBuf<int64_t> dI((size_t)n * k);
+        DevBuf<int32_t> dst((size_t)n * 2);
+        dx.upload(x);
+        hipEvent_t e0, e1;
+        DRM_HIP_CHECK(hipEventCreate(&e0));
+        DRM_HIP_CHECK(hipEventCreate(&e1));
+        DRM_HIP_CHECK(hipEventRecord(e0, nullptr));
+        drm::launch_hnsw_search(index->dev, dx.p, n, k, ef, dD.p, dI.p, dst.p, dst.p + n, nullptr);
+        DRM_HIP_CHECK(hipEventRecord(e1, nullptr));
+        DRM_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        DRM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        dD.download(D);
+        dI.download(I);
+        if (stats) {
+            std::vector<int32_t> st((size_t)n * 2);
+            dst.download(st.data());
+            stats->nq = n;
+            stats->ndis = std::accumulate(st.begin(), st.begin() + n, (int64_t)0);
+            stats->nhops = std::accumulate(st.begin() + n, st.end(), (int64_t)0);
+            stats->kernel_ms = ms;
+        }
+    });
+}
+
+// ------------------------------------------------------------------------------------ SW
+int drm_sw_scores(const uint8_t *s1, const int64_t *off1, const int32_t *len1, const uint8_t *s2,
+                  const int64_t *off2, const int32_t *len2, int64_t npairs, int32_t *scores)
+{
+    return guarded([&] {
+        if (npairs <= 0)
+            return;
+        if (!s1 || !off1 || !len1 || !s2 || !off2 || !len2 || !scores)
+            throw Error(DRM_ERR_ARG, "null argument");
+        int64_t n1 = 0, n2 = 0;
+        int max2 = 0;
+        for (int64_t p = 0; p < npairs; ++p) {
+            if (len1[p] < 0 || len2[p] < 0)
+                throw Error(DRM_ERR_ARG, "negative length");
+            n1 = std::max(n1, off1[p] + len1[p]);
+            n2 = std::max(n2, off2[p] + len2[p]);
+            max2 = std::max(max2, len2[p]);
+        }
+        DevBuf<uint8_t> d1((size_t)std::max<int64_t>(n1, 1)), d2((size_t)std::max<int64_t>(n2, 1));
+        DevBuf<int64_t> do1((size_t)npairs), do2((size_t)npairs);
+        DevBuf<int32_t> dl1((size_t)npairs), dl2((size_t)npairs), ds((size_t)npairs);
+        if (n1)
+            DRM_HIP_CHECK(hipMemcpy(d1.p, s1, (size_t)n1, hipMemcpyHostToDevice));
+        if (n2)
+            DRM_HIP_CHECK(hipMemcpy(d2.p, s2, (size_t)n2, hipMemcpyHostToDevice));
+        do1.upload(off1);
+        do2.upload(off2);
+        dl1.upload(len1);
+        dl2.upload(len2);
+        drm::launch_sw_pairs(d1.p, do1.p, dl1.p, d2.p, do2.p, dl2.p, npairs, ds.p, max2, nullptr);
+        DRM_HIP_CHECK(hipDeviceSynchronize());
+        ds.download(scores);
+    });
+}
+
+int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int64_t row_stride, int device,
+                    drm_refs **out)
+{
+    return guarded([&] {
+        if (!out || (!windows && n_ref > 0))
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (n_ref < 0 || ref_len < 0 || row_stride < ref_len)
+            throw Error(DRM_ERR_ARG, "invalid window table shape");
+        DRM_HIP_CHECK(hipSetDevice(device));
+        std::unique_ptr<drm_refs> r(new drm_refs());
+        r->dev.device = device;
+        r->dev.n_ref = n_ref;
+        r->dev.ref_len = ref_len;
+        r->dev.row_stride = std::max<int64_t>(16, ((int64_t)ref_len + 15) / 16 * 16);
+        const size_t bytes = (size_t)std::max<int64_t>(n_ref, 1) * (size_t)r->dev.row_stride;
+        DRM_HIP_CHECK(hipMalloc(&r->dev.windows, bytes));
+        DRM_HIP_CHECK(hipMemset(r->dev.windows, 0, bytes));
+        if (n_ref > 0) {
+            DRM_HIP_CHECK(hipMemcpy2D(r->dev.windows, (size_t)r->dev.row_stride, windows, (size_t)row_stride,
+                                      (size_t)ref_len, (size_t)n_ref, hipMemcpyHostToDevice));
+        }
+        *out = r.release();
+    });
+}
+
+int drm_refs_free(drm_refs *refs)
+{
+    return guarded([&] {
+        if (!refs)
+            return;
+        (void)hipSetDevice(refs->dev.device);
+        if (refs->dev.windows)
+            (void)hipFree(refs->dev.windows);
+        delete refs;
+    });
+}
+
+static drm::RerankArgs make_rerank_args(drm_refs *refs, const int64_t *nb, int64_t nq, int32_t kk, const uint8_t *q,
+                                        const int32_t *ql, int32_t q_stride, int64_t stride, int32_t k,
+                                        int32_t k_clusters, int32_t *ts, uint64_t *ti, int32_t *st)
+{
+    if (!refs)
+        throw Error(DRM_ERR_ARG, "null refs");
+    if (stride < 1)
+        throw Error(DRM_ERR_ARG, "stride must be >= 1");
+    if (k < 0 || k_clusters < 0 || kk < 0)
+        throw Error(DRM_ERR_ARG, "negative k / k_clusters / kk");
+    if ((int64_t)k > (int64_t)k_clusters * 2 * stride) // post_processor.cpp:486-489
+        throw Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
+    drm::RerankArgs a{};
+    a.refs = refs->dev.windows;
+    a.n_ref = refs->dev.n_ref;
+    a.ref_len = refs->dev.ref_len;
+    a.row_stride = refs->dev.row_stride;
+    a.neighbors = nb;
+    a.kk = kk;
+    a.k_clusters = k_clusters;
+    a.stride = stride;
+    a.queries = q;
+    a.q_len = ql;
+    a.q_stride = q_stride;
+    a.k = k;
+    a.nq = nq;
+    a.top_scores = ts;
+    a.top_ids = ti;
+    a.status = st;
+    return a;
+}
+
+int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                                      int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
+                                      uint64_t *d_top_ids, int32_t *d_status, void *stream)
+{
+    return guarded([&] {
+        drm::RerankArgs a = make_rerank_args(refs, d_neighbors, nq, kk, d_queries, d_q_len, q_stride, stride, k,
+                                             k_clusters, d_top_scores, d_top_ids, d_status);
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        // max query length bounded by the row stride of the query buffer
+        drm::launch_sw_rerank(refs->dev, a, q_stride, (hipStream_t)stream);
+    });
+}
+
+int drm_post_process_sw_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                               int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
+                               int32_t *counts, int64_t *bad_query)
+{
+    return guarded([&] {
+        if (bad_query)
+            *bad_query = -1;
+        if (nq <= 0)
+            return;
+        if (!neighbors || !queries || !q_len || !top_scores || !top_ids || !counts)
+            throw Error(DRM_ERR_ARG, "null argument");
+        int max_q = 0;
+        for (int64_t i = 0; i < nq; ++i) {
+            if (q_len[i] < 0 || q_len[i] > q_stride)
+                throw Error(DRM_ERR_ARG, "query length outside [0, q_stride]");
+            max_q = std::max(max_q, q_len[i]);
+        }
+        drm::RerankArgs a = make_rerank_args(refs, nullptr, nq, kk, nullptr, nullptr, q_stride, stride, k,
+                                             k_clusters, nullptr, nullptr, nullptr);
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        DevBuf<int64_t> dn((size_t)nq * kk);
+        DevBuf<uint8_t> dq((size_t)nq * q_stride);
+        DevBuf<int32_t> dl((size_t)nq), dst((size_t)nq), ds((size_t)nq * k);
+        DevBuf<uint64_t> di((size_t)nq * k);
+        if (dn.n)
+            dn.upload(neighbors);
+        if (dq.n)
+            dq.upload(queries);
+        dl.upload(q_len);
+        a.neighbors = dn.p;
+        a.queries = dq.p;
+        a.q_len = dl.p;
+        a.top_scores = ds.p;
+        a.top_ids = di.p;
+        a.status = dst.p;
+        drm::launch_sw_rerank(refs->dev, a, max_q, nullptr);
+        DRM_HIP_CHECK(hipDeviceSynchronize());
+        std::vector<int32_t> st((size_t)nq);
+        dst.download(st.data());
+        if (ds.n) {
+            ds.download(top_scores);
+            di.download(top_ids);
+        }
+        int64_t first_bad = -1, first_over = -1;
+        for (int64_t i = 0; i < nq; ++i) {
+            counts[i] = st[(size_t)i] > 0 ? st[(size_t)i] : 0;
+            if (st[(size_t)i] == -1 && first_bad < 0)
+                first_bad = i;
+            if ((st[(size_t)i] == -2 || st[(size_t)i] == -3) && first_over < 0)
+                first_over = i;
+        }
+        if (first_over >= 0)
+            throw Error(DRM_ERR_UNSUPPORTED, "query " + std::to_string(first_over) + " expands to more than " +
+                                                 std::to_string(drm::kMaxCands) + " candidates or exceeds the SW length limit");
+        if (first_bad >= 0) {
+            if (bad_query)
+                *bad_query = first_bad;
+            // count the candidates of the offending query for the reference's message
+            const int64_t *nb = neighbors + first_bad * kk;
+            int64_t nc = 0;
+            for (int i = 0; i < std::min(k_clusters, kk); ++i) {
+                uint64_t id = (uint64_t)nb[i];
+                if (stride == 1) {
+                    nc += id < (uint64_t)refs->dev.n_ref;
+                } else {
+                    uint64_t act = id * (uint64_t)stride;
+                    if (act >= (uint64_t)refs->dev.n_ref)
+                        continue;
+                    uint64_t s0 = act >= (uint64_t)(stride - 1) ? act - stride + 1 : 0;
+                    nc += (int64_t)(std::min<uint64_t>(act + stride, refs->dev.n_ref) - s0);
+                }
+            }
+            throw Error(DRM_ERR_CANDS,
+                        "Not enough candidates (" + std::to_string(nc) + " < " + std::to_string(k) + ")");
+        }
+    });
+}
+
+} // extern "C"

@@ -1,0 +1,112 @@
+// deepreadmapper_amd/csrc/drm_device.h -- device-side data structures + kernel launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "drm_internal.h"
+
+#define DRM_HIP_CHECK(expr)                                                                                 \
+    do {                                                                                                    \
+        hipError_t _e = (expr);                                                                             \
+        if (_e != hipSuccess)                                                                               \
+            throw ::drm::Error(DRM_ERR_HIP, std::string(#expr) + " failed: " + hipGetErrorString(_e) + " (" + \
+                                                __FILE__ + ":" + std::to_string(__LINE__) + ")");            \
+    } while (0)
+
+namespace drm {
+
+constexpr int kMaxLevels = 24; // HNSW levels representable in SearchArgs::cum
+
+// HBM image of an IndexHNSWPQ (DESIGN.md "data layout in HBM").
+struct DeviceIndex {
+    int device = 0;
+    int32_t d = 0, pq_M = 0, pq_nbits = 0, dsub = 0, ksub = 0, code_size = 0;
+    int64_t ntotal = 0;
+    int32_t deg0 = 0, n_levels = 0, max_level = -1, entry_point = -1;
+    int32_t cum[kMaxLevels + 1] = {};
+    int32_t has_dup_links = 0; // some neighbour row lists one id twice
+    float *centroids = nullptr;    // [M][ksub][dsub] f32
+    uint8_t *codes = nullptr;      // [ntotal][code_size]
+    int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
+    uint32_t *upper_off = nullptr; // [ntotal] start of node's level>=1 lists in upper_nbr, ~0u if none
+    int32_t *upper_nbr = nullptr;  // concatenated level>=1 lists
+    int64_t upper_len = 0;
+    // search workspace (per resident wave slot), grown on demand
+    int32_t n_slots = 0;
+    int64_t vis_words = 0;         // bitmap words per slot
+    uint32_t *visited = nullptr;   // [n_slots][vis_words]
+    int32_t clear_cap = 0;
+    int32_t *clear_list = nullptr; // [n_slots][clear_cap]
+    uint32_t *counter = nullptr;   // work queue head
+    int64_t device_bytes = 0;
+    HnswPqHost meta; // header fields kept for drm_index_get_info (vectors released)
+};
+
+struct SearchArgs {
+    const float *x;
+    int64_t n;
+    int32_t d, M, nbits, ksub, dsub, code_size;
+    const float *centroids;
+    const uint8_t *codes;
+    const int32_t *nbr0;
+    int32_t deg0;
+    const uint32_t *upper_off;
+    const int32_t *upper_nbr;
+    int32_t cum[kMaxLevels + 1];
+    int32_t max_level, entry_point;
+    int64_t ntotal;
+    int32_t k, efSearch, ef, kpad;
+    float *D;
+    int64_t *I;
+    int32_t *ndis;
+    int32_t *nhops;
+    uint32_t *visited;
+    int64_t vis_words;
+    int32_t *clear_list;
+    int32_t clear_cap;
+    uint32_t *counter;
+    int32_t check_dups;
+};
+
+void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
+                        int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream);
+
+// ---------------------------------------------------------------------------------- SW rerank
+struct DeviceRefs {
+    int device = 0;
+    uint8_t *windows = nullptr; // [n_ref][row_stride], row_stride % 16 == 0
+    int64_t n_ref = 0;
+    int32_t ref_len = 0;
+    int64_t row_stride = 0;
+};
+
+struct RerankArgs {
+    const uint8_t *refs;
+    int64_t n_ref;
+    int32_t ref_len;
+    int64_t row_stride;
+    const int64_t *neighbors;
+    int32_t kk, k_clusters;
+    int64_t stride;
+    const uint8_t *queries;
+    const int32_t *q_len;
+    int32_t q_stride;
+    int32_t k;
+    int64_t nq;
+    int32_t *top_scores;
+    uint64_t *top_ids;
+    int32_t *status;
+};
+
+constexpr int kMaxCands = 1024; // candidates per query kept in LDS
+
+void launch_sw_rerank(const DeviceRefs &refs, const RerankArgs &a, int max_qlen, hipStream_t stream);
+
+// generic batched calc_sw_score: one wave per pair
+void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *d_len1, const uint8_t *d_s2,
+                     const int64_t *d_off2, const int32_t *d_len2, int64_t npairs, int32_t *d_scores, int max_len2,
+                     hipStream_t stream);
+
+} // namespace drm

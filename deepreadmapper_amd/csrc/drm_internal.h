@@ -1,0 +1,105 @@
+// deepreadmapper_amd/csrc/drm_internal.h -- private C++ API shared by the library and the CLIs.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <variant>
+#include <vector>
+
+#include "drm_hip.h"
+
+namespace drm {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string &msg);
+
+// ---------------------------------------------------------------------------------------------
+// Host image of a faiss IndexHNSWPQ: exactly the fields faiss::write_index / read_index touch
+// for fourcc "IHNp" + storage "IxPq" [faiss impl/index_write.cpp, impl/index_read.cpp].
+// ---------------------------------------------------------------------------------------------
+struct IndexHeader {
+    int32_t d = 0;
+    int64_t ntotal = 0;
+    uint8_t is_trained = 1;
+    int32_t metric_type = 1; // METRIC_L2
+    float metric_arg = 0.f;
+};
+
+struct HnswPqHost {
+    IndexHeader hdr;
+    // faiss::HNSW
+    std::vector<double> assign_probas;
+    std::vector<int32_t> cum_nneighbor_per_level;
+    std::vector<int32_t> levels;   // level + 1 per node
+    std::vector<uint64_t> offsets; // ntotal + 1
+    std::vector<int32_t> neighbors;
+    int32_t entry_point = -1;
+    int32_t max_level = -1;
+    int32_t efConstruction = 40;
+    int32_t efSearch = 16;
+    int32_t upper_beam = 1;
+    // storage: faiss::IndexPQ
+    IndexHeader storage_hdr;
+    uint64_t pq_d = 0, pq_M = 0, pq_nbits = 0;
+    std::vector<float> centroids; // [M][ksub][dsub]
+    std::vector<uint8_t> codes;   // [ntotal][code_size]
+    int32_t search_type = 0;
+    uint8_t encode_signs = 0;
+    int32_t polysemous_ht = 0;
+
+    int dsub() const { return pq_M ? int(pq_d / pq_M) : 0; }
+    int ksub() const { return 1 << int(pq_nbits); }
+    int code_size() const { return int((pq_M * pq_nbits + 7) / 8); }
+    int deg0() const { return cum_nneighbor_per_level.size() > 1 ? cum_nneighbor_per_level[1] - cum_nneighbor_per_level[0] : 0; }
+    int nb_at(int level) const { return cum_nneighbor_per_level[level + 1] - cum_nneighbor_per_level[level]; }
+};
+
+HnswPqHost read_hnswpq(const std::string &path);                 // throws Error
+void write_hnswpq(const HnswPqHost &ix, const std::string &path); // throws Error
+void validate_hnswpq(const HnswPqHost &ix);                      // throws Error(DRM_ERR_FORMAT)
+
+// faiss HNSW::set_default_probas(M, 1/log(M)) [faiss impl/HNSW.cpp]
+void hnsw_default_probas(int M, std::vector<double> &probas, std::vector<int32_t> &cum);
+
+// ---------------------------------------------------------------------------------------------
+// Formats (src/utils/utils.cpp, src/utils/parse_inputs.cpp)
+// ---------------------------------------------------------------------------------------------
+using ConfigValue = std::variant<size_t, float, std::string>; // includes/utils/utils.hpp:102
+
+void save_config(const std::unordered_map<std::string, ConfigValue> &config, const std::string &folder,
+                 const std::string &file = "config.txt");
+std::unordered_map<std::string, ConfigValue> load_config(const std::string &path);
+
+// cnpy-compatible npy v1.0 writer/reader (descr '<u8', '<f4', '<i4', ...)
+void npy_save(const std::string &path, const void *data, const std::vector<size_t> &shape, char kind, int itemsize);
+struct NpyArray {
+    std::vector<size_t> shape;
+    char kind = 'f';
+    int itemsize = 4;
+    bool fortran = false;
+    std::vector<uint8_t> bytes;
+};
+NpyArray npy_load(const std::string &path);
+
+std::string reverse_complement(const std::string &seq);
+// format_fasta (parse_inputs.cpp:223-369): fwd/RC interleaved windows; lookup_mode=false adds "<" ">".
+std::vector<std::string> format_fasta(const std::string &data, size_t ref_len, size_t stride, bool lookup_mode);
+// format_fastq (parse_inputs.cpp:843-950): "<"+seq+">" and ids up to ' ', '\t', '/'.
+void format_fastq(const std::string &data, std::vector<std::string> &seqs, std::vector<std::string> &ids);
+// read_file (utils.cpp:188-215) dispatch on extension; .txt = one sequence per non-empty line.
+void read_file(const std::string &path, std::vector<std::string> &seqs, std::vector<std::string> &ids,
+               size_t ref_len = 150, size_t stride = 1, bool lookup_mode = false);
+std::string read_whole_file(const std::string &path);
+
+void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_hnsw, int efc, double sample_rate,
+                  int nthreads, uint64_t seed, const std::string &path);
+void embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len, int64_t n, int dim, uint64_t seed,
+                 float *out);
+constexpr uint64_t kEmbedSeed = 42; // seed of the stand-in embedder used by the CLIs
+
+} // namespace drm

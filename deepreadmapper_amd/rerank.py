@@ -1,0 +1,149 @@
+"""Smith-Waterman rerank: drop-ins for calc_sw_score (src/utils/metrics.cpp:10-45), sw_reranker
+(src/utils/reranker.cpp:3-51) and post_process_sw_static (src/utils/post_processor.cpp:454-549).
+All scoring runs in the HIP kernels of libdrm_hip.so."""
+import ctypes as C
+
+import numpy as np
+
+from ._native import DrmError, DRM_ERR_CANDS, check, lib, ptr
+
+
+def _as_bytes(s):
+    return s.encode() if isinstance(s, str) else bytes(s)
+
+
+def calc_sw_scores(seqs1, seqs2):
+    """Batched calc_sw_score(seqs1[p], seqs2[p])."""
+    a = [_as_bytes(s) for s in seqs1]
+    b = [_as_bytes(s) for s in seqs2]
+    if len(a) != len(b):
+        raise ValueError("length mismatch")
+    n = len(a)
+    if n == 0:
+        return np.zeros(0, dtype=np.int32)
+    buf1 = np.frombuffer(b"".join(a) or b"\0", dtype=np.uint8).copy()
+    buf2 = np.frombuffer(b"".join(b) or b"\0", dtype=np.uint8).copy()
+    l1 = np.array([len(s) for s in a], dtype=np.int32)
+    l2 = np.array([len(s) for s in b], dtype=np.int32)
+    o1 = np.concatenate([[0], np.cumsum(l1[:-1], dtype=np.int64)]).astype(np.int64)
+    o2 = np.concatenate([[0], np.cumsum(l2[:-1], dtype=np.int64)]).astype(np.int64)
+    out = np.empty(n, dtype=np.int32)
+    check(lib().drm_sw_scores(ptr(buf1), ptr(o1), ptr(l1), ptr(buf2), ptr(o2), ptr(l2), n, ptr(out)))
+    return out
+
+
+def calc_sw_score(seq1, seq2):
+    return int(calc_sw_scores([seq1], [seq2])[0])
+
+
+class WindowTable:
+    """Device-resident `ref_seqs` (static lookup table of equal-length windows)."""
+
+    def __init__(self, windows, device=0):
+        if isinstance(windows, np.ndarray):
+            arr = np.ascontiguousarray(windows, dtype=np.uint8)
+        else:
+            ws = [_as_bytes(w) for w in windows]
+            L = len(ws[0]) if ws else 0
+            if any(len(w) != L for w in ws):
+                raise ValueError("static window table needs equal-length windows")
+            arr = np.frombuffer(b"".join(ws), dtype=np.uint8).reshape(len(ws), L) if ws else np.zeros((0, 0), np.uint8)
+        self.n_ref, self.ref_len = arr.shape
+        h = C.c_void_p()
+        check(lib().drm_refs_create(ptr(arr) if arr.size else None, self.n_ref, self.ref_len, self.ref_len,
+                                    int(device), C.byref(h)))
+        self._h = h.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def free(self):
+        if self._h:
+            check(lib().drm_refs_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                lib().drm_refs_free(self._h)
+        except Exception:
+            pass
+
+
+def pack_queries(query_seqs):
+    qs = [_as_bytes(q) for q in query_seqs]
+    stride = max([len(q) for q in qs] + [1])
+    buf = np.zeros((len(qs), stride), dtype=np.uint8)
+    for i, q in enumerate(qs):
+        buf[i, :len(q)] = np.frombuffer(q, dtype=np.uint8)
+    return buf, np.array([len(q) for q in qs], dtype=np.int32)
+
+
+def rerank_arrays(table, neighbors, query_seqs, stride, k, k_clusters):
+    """Array form of post_process_sw_static: returns (scores [nq,k] i32, ids [nq,k] u64, counts [nq])."""
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    nq, kk = nb.shape
+    qbuf, qlen = query_seqs if isinstance(query_seqs, tuple) else pack_queries(query_seqs)
+    scores = np.empty((nq, k), dtype=np.int32)
+    ids = np.empty((nq, k), dtype=np.uint64)
+    counts = np.empty(nq, dtype=np.int32)
+    bad = C.c_int64(-1)
+    rc = lib().drm_post_process_sw_static(table.handle, ptr(nb), nq, kk, ptr(qbuf), ptr(qlen), qbuf.shape[1],
+                                          int(stride), int(k), int(k_clusters), ptr(scores), ptr(ids), ptr(counts),
+                                          C.byref(bad))
+    check(rc)
+    return scores, ids, counts
+
+
+def post_process_sw_static(neighbors, distances, ref_seqs, query_seqs, ref_len, stride, k, k_clusters):
+    """Reference-shaped result: flattened (final_seqs, final_scores, final_ids) over all queries
+    (post_processor.cpp:533-548). Raises RuntimeError like the reference on k / candidate errors."""
+    table = ref_seqs if isinstance(ref_seqs, WindowTable) else WindowTable(ref_seqs)
+    nb = np.asarray([list(r) for r in neighbors], dtype=np.int64) if not isinstance(neighbors, np.ndarray) else neighbors
+    try:
+        scores, ids, counts = rerank_arrays(table, nb, query_seqs, stride, k, k_clusters)
+    except DrmError as e:
+        raise RuntimeError(str(e)) from e
+    seqs, sc, fid = [], [], []
+    for i in range(len(counts)):
+        for j in range(int(counts[i])):
+            wid = int(ids[i, j])
+            sc.append(int(scores[i, j]))
+            fid.append(wid)
+            if not isinstance(ref_seqs, WindowTable):
+                seqs.append(ref_seqs[wid])
+    return seqs, sc, fid
+
+
+def sw_reranker(cand_seqs, cand_ids, query_seq, k):
+    """sw_reranker(cand_seqs, cand_ids, query_seq, k) -> (top_seqs, top_scores, top_ids)."""
+    n = len(cand_seqs)
+    if n == 0 or k == 0:
+        return [], [], []
+    scores = calc_sw_scores(cand_seqs, [query_seq] * n)
+    if n < k:
+        raise RuntimeError(f"Not enough candidates ({n} < {k})")
+    order = partial_sort_order(scores, k)
+    return [cand_seqs[i] for i in order], [int(scores[i]) for i in order], [cand_ids[i] for i in order]
+
+
+def partial_sort_order(scores, k):
+    """std::partial_sort order of reranker.cpp:38-40 computed on the device: the rerank kernel sorts
+    candidate windows of a one-query table whose scores are the given ones."""
+    scores = np.asarray(scores, dtype=np.int32)
+    n = len(scores)
+    # A window table whose window c scores exactly scores[c] against a query of 'A'*m:
+    # window c = 'A'*scores[c] + 'C'*(L - scores[c]) with L = max score (calc_sw_score = run of A's).
+    L = max(int(scores.max()) if n else 0, 1)
+    if scores.min(initial=0) < 0:
+        raise ValueError("scores must be >= 0")
+    win = np.full((n, L), ord("C"), dtype=np.uint8)
+    for c, s in enumerate(scores):
+        win[c, :s] = ord("A")
+    table = WindowTable(win)
+    q = b"A" * L
+    nb = np.arange(n, dtype=np.int64)[None, :]
+    _, ids, _ = rerank_arrays(table, nb, [q], 1, k, n)
+    table.free()
+    return [int(i) for i in ids[0]]

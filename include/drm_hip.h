@@ -1,0 +1,148 @@
+/*
+ * include/drm_hip.h -- C ABI of libdrm_hip.so, the MI355X-native drop-in for DeepReadMapper's
+ * query hot path (HNSW-PQ candidate search + Smith-Waterman rerank).
+ *
+ * Every entry point is plain C: pointers + sizes, no C++/torch types. Return value 0 = success,
+ * negative = error (message via drm_last_error(), thread-local), mirroring the reference's
+ * exception + "Error: ..." convention (src/main.cpp:439-448). All citations are to the reference
+ * (/root/reference, hunglongtrangithub/DeepReadMapper) unless marked [faiss].
+ */
+#ifndef DRM_HIP_H
+#define DRM_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRM_OK 0
+#define DRM_ERR_ARG (-1)       /* bad argument (std::invalid_argument / runtime_error in reference) */
+#define DRM_ERR_IO (-2)        /* file missing / unreadable                                          */
+#define DRM_ERR_FORMAT (-3)    /* index file not an IndexHNSWPQ we can read                          */
+#define DRM_ERR_HIP (-4)       /* HIP runtime error                                                  */
+#define DRM_ERR_CANDS (-5)     /* "Not enough candidates (n < k)"  src/utils/reranker.cpp:26-29      */
+#define DRM_ERR_K (-6)         /* "Final k too large..."           src/utils/post_processor.cpp:486-489 */
+#define DRM_ERR_UNSUPPORTED (-7)
+
+typedef struct drm_index drm_index; /* device-resident IndexHNSWPQ */
+typedef struct drm_refs drm_refs;   /* device-resident static window table (ref_seqs) */
+
+typedef struct {
+    int32_t d;             /* vector dimension                                  */
+    int64_t ntotal;        /* number of indexed vectors                         */
+    int32_t pq_M;          /* PQ sub-quantizers (M_pq)                          */
+    int32_t pq_nbits;      /* bits per sub-quantizer code                       */
+    int32_t M_hnsw;        /* HNSW M; level-0 degree = 2*M_hnsw                 */
+    int32_t max_level;     /* HNSW max_level                                    */
+    int32_t entry_point;   /* HNSW entry point                                  */
+    int32_t efConstruction;
+    int32_t efSearch;      /* value stored in the file                          */
+    int32_t metric_type;   /* 1 = METRIC_L2 (the only one the reference builds) */
+    int64_t device_bytes;  /* HBM held by the index on its device              */
+} drm_index_info;
+
+typedef struct {
+    int64_t nq;            /* queries searched                                       */
+    int64_t ndis;          /* sum of HNSWStats.ndis  [faiss hnsw_stats]               */
+    int64_t nhops;         /* sum of HNSWStats.nhops                                  */
+    double kernel_ms;      /* device time of the search kernel(s) (hipEvent)          */
+} drm_search_stats;
+
+/* ---------------------------------------------------------------- runtime / errors */
+const char *drm_last_error(void);
+int drm_version(void); /* major*10000 + minor*100 + patch */
+int drm_device_count(int *n);
+int drm_set_device(int device);
+int drm_device_sync(void);
+int drm_malloc(void **ptr, size_t bytes);
+int drm_free(void *ptr);
+int drm_memset(void *ptr, int value, size_t bytes);
+int drm_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int drm_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int drm_stream_create(void **stream);
+int drm_stream_destroy(void *stream);
+int drm_stream_sync(void *stream);
+int drm_event_create(void **ev);
+int drm_event_destroy(void *ev);
+int drm_event_record(void *ev, void *stream);
+int drm_event_elapsed_ms(void *start, void *stop, float *ms);
+
+/* ---------------------------------------------------------------- index (search side)
+ * drm_index_load replaces `faiss::read_index(index_file) + dynamic_cast<faiss::IndexHNSWPQ*>`
+ * (src/main.cpp:236-237). It parses the faiss "IHNp" file [faiss impl/index_read.cpp], validates
+ * it, re-lays it out for HBM (dense level-0 rows, compact upper levels) and uploads it to
+ * `device`. drm_index_free replaces `delete alg_hnsw` (src/main.cpp:299). */
+int drm_index_load(const char *path, int device, drm_index **out);
+int drm_index_free(drm_index *index);
+int drm_index_get_info(const drm_index *index, drm_index_info *info);
+
+/* drm_search replaces faiss_search(index, query_data, k, ef) (includes/hnswpq/search.hpp:18-21,
+ * src/hnswpq/search.cpp:6-56), i.e. `index->hnsw.efSearch = ef; index->search(n, x, k, D, I)`.
+ * Host pointers: x [n x d] f32 row-major; D [n x k] f32 and I [n x k] int64 are caller-owned and
+ * filled like faiss (ascending distance, ties by id, missing slots (+inf, -1)).
+ * Throws-equivalent: n == 0 -> DRM_ERR_ARG "Query data is empty" (search.cpp:16-19).
+ * stats may be NULL. */
+int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k, int32_t ef, float *D, int64_t *I,
+               drm_search_stats *stats);
+
+/* Same search on device-resident buffers, enqueued on `stream` (a hipStream_t, NULL = default).
+ * ndis / nhops ([n] int32, may be NULL) receive the per-query HNSWStats the kernel measured. */
+int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                      int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, void *stream);
+
+/* ---------------------------------------------------------------- Smith-Waterman rerank */
+/* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):
+ * pair p scores s1[off1[p] .. +len1[p]) against s2[off2[p] .. +len2[p]). Host pointers. */
+int drm_sw_scores(const uint8_t *s1, const int64_t *off1, const int32_t *len1, const uint8_t *s2,
+                  const int64_t *off2, const int32_t *len2, int64_t npairs, int32_t *scores);
+
+/* The static reference window table `ref_seqs` (read_file(ref, ref_len, 1, lookup=true),
+ * src/main.cpp:190): n_ref windows of ref_len bytes, window r at windows[r*row_stride]. */
+int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int64_t row_stride, int device,
+                    drm_refs **out);
+int drm_refs_free(drm_refs *refs);
+
+/* post_process_sw_static (src/utils/post_processor.cpp:454-549) -> find_sequences (static,
+ * :204-336) -> sw_reranker (src/utils/reranker.cpp:3-51) -> calc_sw_score, for nq queries.
+ *   neighbors [nq x kk] int64 faiss labels (-1 allowed), queries [nq x q_stride] bytes, q_len[nq]
+ *   (the tagged "<"+read+">" strings of format_fastq, src/utils/parse_inputs.cpp:843-950).
+ * Outputs [nq x k]: top_scores (SW score), top_ids (dense window id, size_t), counts[nq] (k, or 0
+ * when the query had no candidate at all: reranker.cpp:10-11). Ordering among equal scores is
+ * libstdc++ std::partial_sort's (reranker.cpp:38-40).
+ * Errors: DRM_ERR_K (k > k_clusters*2*stride), DRM_ERR_CANDS (some query has 0 < n_cands < k;
+ * *bad_query receives the first such query index when bad_query != NULL). Host pointers. */
+int drm_post_process_sw_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                               int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
+                               int32_t *counts, int64_t *bad_query);
+
+/* Device-buffer form, enqueued on `stream`. d_status[nq] receives per-query status
+ * (k or 0 = rows emitted, -1 = not enough candidates, -2 = more than 1024 candidates,
+ * -3 = query longer than q_stride's SW build). Host must check d_status. */
+int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                                      int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
+                                      uint64_t *d_top_ids, int32_t *d_status, void *stream);
+
+/* ---------------------------------------------------------------- index build (hnswpq_index)
+ * build_faiss_index (src/hnswpq/index.cpp:86-193): trains PQ on an evenly spaced sample of
+ * sample_rate*n vectors (create_training_set :57-84, Config::Build::SAMPLE_RATE = 0.5), builds the
+ * HNSW graph (M_hnsw, efConstruction) with PQ-ADC distances and writes a faiss "IHNp" file.
+ * nthreads <= 0 -> all cores; nthreads == 1 gives a deterministic graph. */
+int drm_build_hnswpq(const float *x, int64_t n, int32_t d, int32_t M_pq, int32_t nbits, int32_t M_hnsw,
+                     int32_t efConstruction, double sample_rate, int32_t nthreads, uint64_t seed,
+                     const char *index_path);
+
+/* ---------------------------------------------------------------- synthetic embedder
+ * Stand-in for the OpenVINO read encoder (Vectorizer::vectorize, src/inference/vectorize.cpp:34-141,
+ * OUT OF SCOPE): e(s) = normalize(sum_t R[3-mer(s, t)]) over ACGT 3-mers, R a [64 x dim] N(0,1)
+ * matrix drawn from splitmix64(seed). Deterministic; used by the CLIs and the synthetic workloads so
+ * that reads land near their source windows. seqs: n strings at seqs[off[i] .. +len[i]). */
+int drm_embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len, int64_t n, int32_t dim,
+                    uint64_t seed, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

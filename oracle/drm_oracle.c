@@ -1,0 +1,614 @@
+/*
+ * oracle/drm_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's query hot path, used (a) as the parity checker for the HIP
+ * path and (b) as the OpenMP CPU baseline timed by bench.py. Never linked into the product.
+ * Compile with -ffp-contract=off: every fp32 product/sum below is rounded separately, in the
+ * order written, which is the order the HIP kernels use (DESIGN.md "fixed fp32 op order").
+ *
+ * Citations are to /root/reference (DeepReadMapper) unless marked [upstream faiss], in which case
+ * the code restates faiss >= 1.8 semantics (faiss is not vendored in the reference nor installed
+ * here): faiss/impl/HNSW.cpp, faiss/utils/Heap.h, faiss/IndexHNSW.cpp,
+ * faiss/IndexPQ.cpp, faiss/impl/ProductQuantizer.cpp, faiss/impl/code_distance/.
+ */
+#include "drm_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static inline int imax(int a, int b) { return a > b ? a : b; }
+
+/* ========================================================================================
+ * Smith-Waterman score. Restates calc_sw_score, src/utils/metrics.cpp:10-45:
+ *   match +1, mismatch -1, linear gap -1 (:18-20), dp[i][j] = max(0, diag+s, up-1, left-1)
+ *   (:30-41), running max over all cells. Raw byte equality (case-sensitive, 'N'=='N').
+ * The full (len1+1)x(len2+1) matrix of :26 is replaced by one rolling row: same values.
+ * ====================================================================================== */
+int oracle_calc_sw_score(const uint8_t *s1, int64_t len1, const uint8_t *s2, int64_t len2)
+{
+    if (len1 <= 0 || len2 <= 0)
+        return 0;
+    int stack_row[1024];
+    int *row = (len2 + 1 <= 1024) ? stack_row : (int *)malloc(sizeof(int) * (size_t)(len2 + 1));
+    for (int64_t j = 0; j <= len2; ++j)
+        row[j] = 0;
+    int best = 0;
+    for (int64_t i = 1; i <= len1; ++i) {
+        const uint8_t c1 = s1[i - 1];
+        int diag = 0; /* dp[i-1][0] */
+        int left = 0; /* dp[i][0]   */
+        for (int64_t j = 1; j <= len2; ++j) {
+            const int up = row[j];
+            const int sm = diag + (c1 == s2[j - 1] ? 1 : -1);
+            int h = imax(imax(0, sm), imax(up - 1, left - 1));
+            diag = up;
+            row[j] = h;
+            left = h;
+            best = imax(best, h);
+        }
+    }
+    if (row != stack_row)
+        free(row);
+    return best;
+}
+
+/* ========================================================================================
+ * libstdc++ std::partial_sort with comp(a, b) := scores[a] > scores[b], the exact call of
+ * src/utils/reranker.cpp:38-40. Restates __partial_sort = __heap_select + __sort_heap and the
+ * helpers __make_heap / __adjust_heap / __push_heap / __pop_heap (bits/stl_heap.h,
+ * bits/stl_algo.h, GCC 11). Tie order among equal scores follows the heap mechanics exactly.
+ * ====================================================================================== */
+#define PS_COMP(a, b) (scores[(a)] > scores[(b)])
+
+static void ps_adjust_heap(int64_t *first, int64_t hole, int64_t len, int64_t value, const int32_t *scores)
+{
+    const int64_t top = hole;
+    int64_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (PS_COMP(first[second], first[second - 1]))
+            second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    /* __push_heap(first, hole, top, value) with comp(*parent, value) */
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top && PS_COMP(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+static void ps_make_heap(int64_t *first, int64_t len, const int32_t *scores)
+{
+    if (len < 2)
+        return;
+    int64_t parent = (len - 2) / 2;
+    for (;;) {
+        int64_t value = first[parent];
+        ps_adjust_heap(first, parent, len, value, scores);
+        if (parent == 0)
+            return;
+        parent--;
+    }
+}
+
+/* __pop_heap(first, first+len, result) */
+static void ps_pop_heap(int64_t *first, int64_t len, int64_t *result, const int32_t *scores)
+{
+    int64_t value = *result;
+    *result = first[0];
+    ps_adjust_heap(first, 0, len, value, scores);
+}
+
+void oracle_partial_sort_desc(int64_t *idx, int64_t n, int64_t k, const int32_t *scores)
+{
+    if (k <= 0)
+        return;
+    /* __heap_select(first, middle, last) */
+    ps_make_heap(idx, k, scores);
+    for (int64_t i = k; i < n; ++i)
+        if (PS_COMP(idx[i], idx[0]))
+            ps_pop_heap(idx, k, idx + i, scores);
+    /* __sort_heap(first, middle) */
+    int64_t last = k;
+    while (last > 1) {
+        --last;
+        ps_pop_heap(idx, last, idx + last, scores);
+    }
+}
+
+/* ========================================================================================
+ * post_process_sw_static (src/utils/post_processor.cpp:454-549) + find_sequences static
+ * (:204-336) + sw_reranker (src/utils/reranker.cpp:3-51).
+ * ====================================================================================== */
+static int64_t pp_one_query(const int64_t *nb, int64_t kk, const uint8_t *refs, int64_t n_ref, int64_t ref_len,
+                            int64_t ref_stride, const uint8_t *q, int32_t qlen, int64_t stride, int64_t k,
+                            int64_t k_clusters, int32_t *out_scores, uint64_t *out_ids)
+{
+    /* :494-495  first min(k_clusters, n_i) neighbour ids, converted long -> size_t (:339-355) */
+    const int64_t nsel = k_clusters < kk ? k_clusters : kk;
+    int64_t cap = (stride == 1) ? (nsel > 0 ? nsel : 1) : (nsel * (2 * stride) + 1);
+    uint64_t *cand = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)cap);
+    int64_t ncand = 0;
+    if (stride == 1) {
+        /* dense branch :215-236 -- ids >= ref_seqs.size() (e.g. -1 -> 2^64-1) are dropped */
+        for (int64_t i = 0; i < nsel; ++i) {
+            uint64_t id = (uint64_t)nb[i];
+            if (id < (uint64_t)n_ref)
+                cand[ncand++] = id;
+        }
+    } else {
+        /* sparse branch :238-335: expand sparse_id*stride to [pos-stride+1, pos+stride), the
+         * mapping keeps every expansion (duplicates included) in original order. */
+        for (int64_t i = 0; i < nsel; ++i) {
+            uint64_t actual = (uint64_t)nb[i] * (uint64_t)stride; /* size_t arithmetic, wraps */
+            if (actual >= (uint64_t)n_ref)
+                continue;
+            uint64_t start = (actual >= (uint64_t)(stride - 1)) ? actual - (uint64_t)stride + 1 : 0;
+            uint64_t end = actual + (uint64_t)stride;
+            if (end > (uint64_t)n_ref)
+                end = (uint64_t)n_ref;
+            for (uint64_t pos = start; pos < end; ++pos)
+                cand[ncand++] = pos;
+        }
+    }
+    if (ncand == 0 || k == 0) { /* reranker.cpp:10-11 returns empty: the query contributes 0 rows */
+        free(cand);
+        return 0;
+    }
+    int32_t *scores = (int32_t *)malloc(sizeof(int32_t) * (size_t)ncand);
+    for (int64_t c = 0; c < ncand; ++c)
+        scores[c] = oracle_calc_sw_score(refs + cand[c] * (uint64_t)ref_stride, ref_len, q, qlen);
+    if (ncand < k) { /* reranker.cpp:26-29 */
+        free(scores);
+        free(cand);
+        return -1;
+    }
+    int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)ncand);
+    for (int64_t c = 0; c < ncand; ++c)
+        idx[c] = c;
+    oracle_partial_sort_desc(idx, ncand, k, scores);
+    for (int64_t j = 0; j < k; ++j) {
+        out_scores[j] = scores[idx[j]];
+        out_ids[j] = cand[idx[j]];
+    }
+    free(idx);
+    free(scores);
+    free(cand);
+    return k;
+}
+
+int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *refs,
+                                      int64_t n_ref, int64_t ref_len, int64_t ref_stride, const uint8_t *queries,
+                                      const int32_t *q_len, int64_t q_stride, int64_t stride, int64_t k,
+                                      int64_t k_clusters, int nthreads, int32_t *top_scores, uint64_t *top_ids,
+                                      int32_t *counts)
+{
+    if (k > k_clusters * 2 * stride) /* :486-489 */
+        return -1000000000;
+    int64_t first_bad = -1;
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic)
+#endif
+    for (int64_t i = 0; i < nq; ++i) {
+        for (int64_t j = 0; j < k; ++j) {
+            top_scores[i * k + j] = -1;
+            top_ids[i * k + j] = UINT64_MAX;
+        }
+        int64_t r = pp_one_query(neighbors + i * kk, kk, refs, n_ref, ref_len, ref_stride, queries + i * q_stride,
+                                 q_len[i], stride, k, k_clusters, top_scores + i * k, top_ids + i * k);
+        counts[i] = r < 0 ? 0 : (int32_t)r;
+        if (r < 0) {
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+            {
+                if (first_bad < 0 || i < first_bad)
+                    first_bad = i;
+            }
+        }
+    }
+    return first_bad >= 0 ? -(1 + first_bad) : 0;
+}
+
+/* ========================================================================================
+ * faiss IndexHNSWPQ search [upstream faiss >= 1.8].
+ * ====================================================================================== */
+
+/* faiss::CMax<T,TI>::cmp2 -- (a1 > b1) || (a1 == b1 && a2 > b2) */
+#define CMP2(v1, v2, i1, i2) (((v1) > (v2)) || (((v1) == (v2)) && ((i1) > (i2))))
+
+/* faiss/utils/Heap.h heap_push<CMax<float,int32>> (1-based internally) */
+static void heap_push_i32(size_t k, float *bh_val, int32_t *bh_ids, float val, int32_t id)
+{
+    bh_val--;
+    bh_ids--;
+    size_t i = k, i_father;
+    while (i > 1) {
+        i_father = i >> 1;
+        if (!CMP2(val, bh_val[i_father], id, bh_ids[i_father]))
+            break;
+        bh_val[i] = bh_val[i_father];
+        bh_ids[i] = bh_ids[i_father];
+        i = i_father;
+    }
+    bh_val[i] = val;
+    bh_ids[i] = id;
+}
+
+/* faiss/utils/Heap.h heap_pop<CMax<float,int32>> */
+static void heap_pop_i32(size_t k, float *bh_val, int32_t *bh_ids)
+{
+    bh_val--;
+    bh_ids--;
+    float val = bh_val[k];
+    int32_t id = bh_ids[k];
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k)
+            break;
+        if ((i2 == k + 1) || CMP2(bh_val[i1], bh_val[i2], bh_ids[i1], bh_ids[i2])) {
+            if (CMP2(val, bh_val[i1], id, bh_ids[i1]))
+                break;
+            bh_val[i] = bh_val[i1];
+            bh_ids[i] = bh_ids[i1];
+            i = i1;
+        } else {
+            if (CMP2(val, bh_val[i2], id, bh_ids[i2]))
+                break;
+            bh_val[i] = bh_val[i2];
+            bh_ids[i] = bh_ids[i2];
+            i = i2;
+        }
+    }
+    bh_val[i] = bh_val[k];
+    bh_ids[i] = bh_ids[k];
+}
+
+/* faiss/utils/Heap.h heap_replace_top<CMax<float,int64>> */
+static void heap_replace_top_i64(size_t k, float *bh_val, int64_t *bh_ids, float val, int64_t id)
+{
+    bh_val--;
+    bh_ids--;
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k)
+            break;
+        if ((i2 == k + 1) || CMP2(bh_val[i1], bh_val[i2], bh_ids[i1], bh_ids[i2])) {
+            if (CMP2(val, bh_val[i1], id, bh_ids[i1]))
+                break;
+            bh_val[i] = bh_val[i1];
+            bh_ids[i] = bh_ids[i1];
+            i = i1;
+        } else {
+            if (CMP2(val, bh_val[i2], id, bh_ids[i2]))
+                break;
+            bh_val[i] = bh_val[i2];
+            bh_ids[i] = bh_ids[i2];
+            i = i2;
+        }
+    }
+    bh_val[i] = val;
+    bh_ids[i] = id;
+}
+
+/* heap_pop<CMax<float,int64>> used by heap_reorder */
+static void heap_pop_i64(size_t k, float *bh_val, int64_t *bh_ids)
+{
+    bh_val--;
+    bh_ids--;
+    float val = bh_val[k];
+    int64_t id = bh_ids[k];
+    size_t i = 1, i1, i2;
+    for (;;) {
+        i1 = i << 1;
+        i2 = i1 + 1;
+        if (i1 > k)
+            break;
+        if ((i2 == k + 1) || CMP2(bh_val[i1], bh_val[i2], bh_ids[i1], bh_ids[i2])) {
+            if (CMP2(val, bh_val[i1], id, bh_ids[i1]))
+                break;
+            bh_val[i] = bh_val[i1];
+            bh_ids[i] = bh_ids[i1];
+            i = i1;
+        } else {
+            if (CMP2(val, bh_val[i2], id, bh_ids[i2]))
+                break;
+            bh_val[i] = bh_val[i2];
+            bh_ids[i] = bh_ids[i2];
+            i = i2;
+        }
+    }
+    bh_val[i] = bh_val[k];
+    bh_ids[i] = bh_ids[k];
+}
+
+/* faiss/utils/Heap.h heap_reorder<CMax<float,int64>> */
+static void heap_reorder_i64(size_t k, float *bh_val, int64_t *bh_ids)
+{
+    size_t i, ii;
+    for (i = 0, ii = 0; i < k; i++) {
+        float val = bh_val[0];
+        int64_t id = bh_ids[0];
+        heap_pop_i64(k - i, bh_val, bh_ids);
+        bh_val[k - ii - 1] = val;
+        bh_ids[k - ii - 1] = id;
+        if (id != -1)
+            ii++;
+    }
+    memmove(bh_val, bh_val + k - ii, ii * sizeof(*bh_val));
+    memmove(bh_ids, bh_ids + k - ii, ii * sizeof(*bh_ids));
+    for (; ii < k; ii++) {
+        bh_val[ii] = INFINITY;
+        bh_ids[ii] = -1;
+    }
+}
+
+/* HNSW::MinimaxHeap [upstream faiss/impl/HNSW.{h,cpp}] */
+typedef struct {
+    int n, k, nvalid;
+    int32_t *ids;
+    float *dis;
+} minimax_t;
+
+static void mm_push(minimax_t *h, int32_t i, float v)
+{
+    if (h->k == h->n) {
+        if (v >= h->dis[0])
+            return;
+        if (h->ids[0] != -1)
+            --h->nvalid;
+        heap_pop_i32((size_t)h->k--, h->dis, h->ids);
+    }
+    heap_push_i32((size_t)++h->k, h->dis, h->ids, v, i);
+    ++h->nvalid;
+}
+
+/* pop_min: minimum dis among valid slots, ties -> highest slot index (the scalar version scans
+ * from k-1 down with strict <; the AVX2 version tracks the rightmost min -- same result). */
+static int32_t mm_pop_min(minimax_t *h, float *vmin_out)
+{
+    int i = h->k - 1;
+    while (i >= 0) {
+        if (h->ids[i] != -1)
+            break;
+        i--;
+    }
+    if (i == -1)
+        return -1;
+    int imin = i;
+    float vmin = h->dis[i];
+    i--;
+    while (i >= 0) {
+        if (h->ids[i] != -1 && h->dis[i] < vmin) {
+            vmin = h->dis[i];
+            imin = i;
+        }
+        i--;
+    }
+    if (vmin_out)
+        *vmin_out = vmin;
+    int32_t ret = h->ids[imin];
+    h->ids[imin] = -1;
+    --h->nvalid;
+    return ret;
+}
+
+/* count_below: counts every slot < k (popped ones included) with dis < thresh */
+static int mm_count_below(const minimax_t *h, float thresh)
+{
+    int n_below = 0;
+    for (int i = 0; i < h->k; i++)
+        if (h->dis[i] < thresh)
+            n_below++;
+    return n_below;
+}
+
+/* PQ code reader: faiss PQDecoder8 / PQDecoderGeneric (LSB-first bit packing). */
+static inline uint32_t pq_decode(const uint8_t *code, int m, int nbits)
+{
+    if (nbits == 8)
+        return code[m];
+    uint64_t bitpos = (uint64_t)m * (uint64_t)nbits;
+    uint64_t byte = bitpos >> 3;
+    int shift = (int)(bitpos & 7);
+    uint64_t acc = 0;
+    int need = shift + nbits;
+    for (int b = 0; b * 8 < need; ++b)
+        acc |= (uint64_t)code[byte + b] << (8 * b);
+    return (uint32_t)((acc >> shift) & ((1ull << nbits) - 1));
+}
+
+void oracle_pq_distance_table(const oracle_hnswpq_t *ix, const float *x, float *lut)
+{
+    const int M = ix->pq_M, ksub = ix->ksub, dsub = ix->dsub;
+    for (int m = 0; m < M; ++m) {
+        const float *xs = x + (size_t)m * dsub;
+        for (int c = 0; c < ksub; ++c) {
+            const float *cen = ix->centroids + ((size_t)m * ksub + c) * dsub;
+            float acc = 0.0f;
+            for (int t = 0; t < dsub; ++t) {
+                float diff = xs[t] - cen[t];
+                float sq = diff * diff;
+                acc = acc + sq;
+            }
+            lut[(size_t)m * ksub + c] = acc;
+        }
+    }
+}
+
+/* distance_single_code / distance_four_codes for M < 16: sequential fp32 sum from 0 */
+static inline float pq_dis(const oracle_hnswpq_t *ix, const float *lut, int64_t node)
+{
+    const uint8_t *code = ix->codes + (size_t)node * ix->code_size;
+    float r = 0.0f;
+    for (int m = 0; m < ix->pq_M; ++m)
+        r = r + lut[(size_t)m * ix->ksub + pq_decode(code, m, ix->pq_nbits)];
+    return r;
+}
+
+typedef struct {
+    float *lut;
+    uint8_t *visited;
+    uint8_t visno;
+    minimax_t cand;
+} hnsw_scratch_t;
+
+/* HNSW::search + greedy_update_nearest + search_from_candidates (level 0, bounded queue,
+ * check_relative_distance = true, upper_beam = 1, no IDSelector). */
+static void hnsw_search_one(const oracle_hnswpq_t *ix, const float *x, int k, int efSearch, float *D, int64_t *I,
+                            int32_t *ndis_out, int32_t *nhops_out, hnsw_scratch_t *s)
+{
+    int64_t ndis = 0, nhops = 0;
+    /* HeapBlockResultHandler::SingleResultHandler::begin: heap_heapify(k) -> (+inf, -1) */
+    for (int j = 0; j < k; ++j) {
+        D[j] = INFINITY;
+        I[j] = -1;
+    }
+    float threshold = D[0];
+
+    if (ix->entry_point == -1 || ix->ntotal == 0) {
+        heap_reorder_i64((size_t)k, D, I);
+        *ndis_out = 0;
+        *nhops_out = 0;
+        return;
+    }
+    oracle_pq_distance_table(ix, x, s->lut); /* PQDistanceComputer::set_query */
+
+    int32_t nearest = ix->entry_point;
+    float d_nearest = pq_dis(ix, s->lut, nearest);
+
+    for (int level = ix->max_level; level >= 1; level--) {
+        /* greedy_update_nearest */
+        for (;;) {
+            int32_t prev_nearest = nearest;
+            size_t o = ix->offsets[nearest];
+            size_t begin = o + (size_t)ix->cum_nneighbor_per_level[level];
+            size_t end = o + (size_t)ix->cum_nneighbor_per_level[level + 1];
+            for (size_t j = begin; j < end; j++) {
+                int32_t v = ix->neighbors[j];
+                if (v < 0)
+                    break;
+                ndis += 1;
+                float dis = pq_dis(ix, s->lut, v);
+                if (dis < d_nearest) {
+                    nearest = v;
+                    d_nearest = dis;
+                }
+            }
+            nhops += 1;
+            if (nearest == prev_nearest)
+                break;
+        }
+    }
+
+    const int ef = efSearch > k ? efSearch : k;
+    minimax_t *cand = &s->cand;
+    cand->n = ef;
+    cand->k = 0;
+    cand->nvalid = 0;
+    mm_push(cand, nearest, d_nearest);
+
+    /* search_from_candidates(level 0) */
+    for (int i = 0; i < cand->nvalid; i++) {
+        int32_t v1 = cand->ids[i];
+        float d = cand->dis[i];
+        if (d < threshold) {
+            heap_replace_top_i64((size_t)k, D, I, d, v1);
+            threshold = D[0];
+        }
+        s->visited[v1] = s->visno;
+    }
+
+    int nstep = 0;
+    const size_t deg0 = (size_t)(ix->cum_nneighbor_per_level[1] - ix->cum_nneighbor_per_level[0]);
+    while (cand->nvalid > 0) {
+        float d0 = 0;
+        int32_t v0 = mm_pop_min(cand, &d0);
+        int n_dis_below = mm_count_below(cand, d0);
+        if (n_dis_below >= efSearch)
+            break;
+        size_t begin = ix->offsets[v0] + (size_t)ix->cum_nneighbor_per_level[0];
+        size_t end = begin + deg0;
+        threshold = D[0];
+        for (size_t j = begin; j < end; j++) {
+            int32_t v1 = ix->neighbors[j];
+            if (v1 < 0)
+                break;
+            int vget = s->visited[v1] == s->visno;
+            s->visited[v1] = s->visno;
+            if (vget)
+                continue;
+            float dis = pq_dis(ix, s->lut, v1);
+            ndis += 1;
+            /* add_to_heap */
+            if (dis < threshold) {
+                heap_replace_top_i64((size_t)k, D, I, dis, v1);
+                threshold = D[0];
+            }
+            mm_push(cand, v1, dis);
+        }
+        nstep++;
+    }
+    nhops += nstep;
+
+    /* VisitedTable::advance */
+    s->visno++;
+    if (s->visno == 250) {
+        memset(s->visited, 0, (size_t)ix->ntotal);
+        s->visno = 1;
+    }
+    /* SingleResultHandler::end -> heap_reorder */
+    heap_reorder_i64((size_t)k, D, I);
+    *ndis_out = (int32_t)ndis;
+    *nhops_out = (int32_t)nhops;
+}
+
+int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, int k, int efSearch, float *D,
+                         int64_t *I, int32_t *ndis, int32_t *nhops, int nthreads)
+{
+    if (k <= 0)
+        return -1;
+    const int ef = efSearch > k ? efSearch : k;
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        hnsw_scratch_t s;
+        s.lut = (float *)malloc(sizeof(float) * (size_t)ix->pq_M * (size_t)ix->ksub);
+        s.visited = (uint8_t *)calloc((size_t)(ix->ntotal > 0 ? ix->ntotal : 1), 1);
+        s.visno = 1;
+        s.cand.ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)ef);
+        s.cand.dis = (float *)malloc(sizeof(float) * (size_t)ef);
+#ifdef _OPENMP
+#pragma omp for schedule(guided)
+#endif
+        for (int64_t i = 0; i < n; ++i)
+            hnsw_search_one(ix, x + i * ix->d, k, efSearch, D + i * k, I + i * k, ndis + i, nhops + i, &s);
+        free(s.lut);
+        free(s.visited);
+        free(s.cand.ids);
+        free(s.cand.dis);
+    }
+    return 0;
+}

@@ -1,0 +1,193 @@
+"""GPU parity tests: the HIP path (through the C ABI) vs the oracle restatement and the golden
+vectors. Integer work (SW scores, top-k ids, ndis/nhops) must be bit-exact; fp32 distances are
+bit-exact too because kernel and oracle use the same op order (tolerance: 0 ulp)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, read_fastq_tagged
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------------------------------ SW
+def test_sw_kat_gpu():
+    from deepreadmapper_amd import calc_sw_scores
+    kat = json.load(open(os.path.join(GOLDEN, "sw_kat.json")))
+    quer = [l.strip() for l in open(os.path.join(GOLDEN, "test_data_quer.txt")).read().splitlines() if l.strip()]
+    got = calc_sw_scores([quer[i] for i, _ in kat["harness_pairs"]], [quer[j] for _, j in kat["harness_pairs"]])
+    assert got.tolist() == kat["harness_scores"]
+    for group in ("edge_cases", "random_pairs"):
+        pairs = kat[group]
+        got = calc_sw_scores([a for a, _, _ in pairs], [b for _, b, _ in pairs])
+        assert got.tolist() == [s for _, _, s in pairs], group
+
+
+def _c1_refs():
+    return np.frombuffer(b"".join(l.strip() for l in open(os.path.join(GOLDEN, "test_data_ref.txt"), "rb")
+                                  if l.strip()), dtype=np.uint8).reshape(1702, 150)
+
+
+def test_sw_c1_matrix_through_rerank_kernel():
+    """Every read of test_data.fastq against every window, through the rerank kernel (k = all
+    candidates), equals the reference-built matrix in the libstdc++ partial_sort order."""
+    from deepreadmapper_amd import WindowTable, rerank_arrays
+    mat = np.load(os.path.join(GOLDEN, "sw_c1_matrix.npy")).astype(np.int32)
+    reads = read_fastq_tagged(os.path.join(GOLDEN, "test_data.fastq"))
+    table = WindowTable(_c1_refs())
+    for lo, hi in ((0, 1000), (1000, 1702)):
+        nb = np.tile(np.arange(lo, hi, dtype=np.int64), (len(reads), 1))
+        sc, ids, cnt = rerank_arrays(table, nb, reads, 1, hi - lo, hi - lo)
+        assert (cnt == hi - lo).all()
+        for i in range(len(reads)):
+            order = O.stl_partial_sort_desc(mat[i, lo:hi], hi - lo)
+            assert ids[i].astype(np.int64).tolist() == (order + lo).tolist()
+            assert sc[i].tolist() == mat[i, lo:hi][order].tolist()
+
+
+def _rerank_both(refs, nb, reads, stride, k, kc):
+    from deepreadmapper_amd import WindowTable, rerank_arrays
+    from deepreadmapper_amd.rerank import pack_queries
+    qbuf, ql = pack_queries(reads)
+    rc, sc_o, id_o, cnt_o = O.post_process_sw_static(nb, refs, refs.shape[1], qbuf, ql, stride, k, kc)
+    assert rc == 0
+    sc, ids, cnt = rerank_arrays(WindowTable(refs), nb, (qbuf, ql), stride, k, kc)
+    assert np.array_equal(cnt, cnt_o)
+    for i in range(len(nb)):
+        n = cnt[i]
+        assert np.array_equal(sc[i, :n], sc_o[i, :n]) and np.array_equal(ids[i, :n], id_o[i, :n]), i
+
+
+def test_rerank_dense_vs_oracle(c1):
+    D, I, _, _ = O.hnswpq_search(c1["fx"], c1["q"], 128, 128)
+    _rerank_both(c1["refs"], I, c1["reads"], 1, 128, 128)
+    _rerank_both(c1["refs"], I, c1["reads"], 1, 10, 40)  # k < k_clusters
+
+
+@pytest.mark.parametrize("stride", [2, 3, 4])
+def test_rerank_sparse_vs_oracle(c1, stride):
+    rng = np.random.default_rng(stride)
+    nb = rng.integers(-1, 1702 // stride + 40, size=(60, 8)).astype(np.int64)
+    _rerank_both(c1["refs"], nb, c1["reads"][:60], stride, 5, 5)
+
+
+def test_rerank_errors(c1):
+    from deepreadmapper_amd import WindowTable, rerank_arrays, DrmError, post_process_sw_static
+    from deepreadmapper_amd._native import DRM_ERR_CANDS, DRM_ERR_K
+    t = WindowTable(c1["refs"])
+    nb = np.arange(8, dtype=np.int64)[None]
+    with pytest.raises(DrmError) as e:
+        rerank_arrays(t, nb, c1["reads"][:1], 1, 17, 8)
+    assert e.value.code == DRM_ERR_K
+    nb2 = np.array([[0, 1, -1, 5, 99999]], dtype=np.int64)
+    with pytest.raises(DrmError) as e:
+        rerank_arrays(t, nb2, c1["reads"][:1], 1, 4, 5)
+    assert e.value.code == DRM_ERR_CANDS and "Not enough candidates (3 < 4)" in str(e.value)
+    sc, ids, cnt = rerank_arrays(t, np.full((2, 5), -1, np.int64), c1["reads"][:2], 1, 4, 5)
+    assert cnt.tolist() == [0, 0]
+    with pytest.raises(RuntimeError, match="Not enough candidates"):
+        post_process_sw_static(nb2, None, list(map(bytes, c1["refs"])), c1["reads"][:1], 150, 1, 4, 5)
+
+
+def test_sw_reranker_api():
+    from deepreadmapper_amd import sw_reranker
+    cands = ["ACGTACGTAA", "TTTT", "ACGTACGTAC", "ACG", "ACGTACGTAC"]
+    seqs, scores, ids = sw_reranker(cands, [10, 11, 12, 13, 14], "<ACGTACGTAC>", 3)
+    exp_scores = [O.calc_sw_score(c.encode(), b"<ACGTACGTAC>") for c in cands]
+    order = O.stl_partial_sort_desc(np.array(exp_scores, np.int32), 3).tolist()
+    assert ids == [[10, 11, 12, 13, 14][i] for i in order] and scores == [exp_scores[i] for i in order]
+    with pytest.raises(RuntimeError, match="Not enough candidates"):
+        sw_reranker(cands, [1, 2, 3, 4, 5], "ACGT", 6)
+
+
+# ------------------------------------------------------------------------------------------ search
+def _search_both(index_path, fx, q, k, ef):
+    from deepreadmapper_amd import read_index
+    ix = read_index(index_path)
+    D, I, st = ix.search(q, k, ef)
+    Do, Io, nd, nh = O.hnswpq_search(fx, q, k, ef)
+    assert np.array_equal(I, Io)
+    assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))  # 0-ulp fp32
+    assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+    ix.free()
+    return D, I
+
+
+@pytest.mark.parametrize("k,ef", [(128, 128), (5, 128), (10, 16), (1, 1), (200, 64), (64, 300)])
+def test_search_c1_bitexact(c1, k, ef):
+    _search_both(c1["index"], c1["fx"], c1["q"], k, ef)
+
+
+def test_search_c1_random_and_exhaustive(c1):
+    rng = np.random.default_rng(9)
+    q = rng.standard_normal((64, 128)).astype(np.float32)
+    _search_both(c1["index"], c1["fx"], q, 32, 96)
+    _search_both(c1["index"], c1["fx"], c1["q"][:40], 50, 2048)  # ef >= ntotal
+
+
+def test_search_syn20k_bitexact(syn20k):
+    w = syn20k["w"]
+    _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
+
+
+def test_search_device_stats(syn20k):
+    from deepreadmapper_amd import read_index
+    from deepreadmapper_amd.device import DeviceBuffer, synchronize
+    w = syn20k["w"]
+    q = w.q_emb[:500]
+    ix = read_index(syn20k["index"])
+    dq = DeviceBuffer.from_host(q)
+    dD, dI = DeviceBuffer((500, 128), np.float32), DeviceBuffer((500, 128), np.int64)
+    nd, nh = DeviceBuffer(500, np.int32), DeviceBuffer(500, np.int32)
+    ix.search_device(dq, 500, 128, 128, dD, dI, nd, nh)
+    synchronize()
+    Do, Io, ndo, nho = O.hnswpq_search(syn20k["fx"], q, 128, 128)
+    assert np.array_equal(dI.download(), Io) and np.array_equal(nd.download(), ndo)
+    assert np.array_equal(nh.download(), nho)
+
+
+def test_faiss_search_api(c1):
+    from deepreadmapper_amd import faiss_search, read_index
+    ix = read_index(c1["index"])
+    ids, dists = faiss_search(ix, c1["q"][:3].tolist(), 7, 32)
+    assert len(ids) == 3 and all(len(r) == 7 for r in ids) and len(dists[0]) == 7
+    with pytest.raises(RuntimeError, match="Query data is empty"):
+        faiss_search(ix, [], 7, 32)
+
+
+# ------------------------------------------------------------------------------------------ CLI
+def test_pipeline_cli_c1(tmp_path, c1):
+    """bin/hnswpq_index + bin/pipeline on the C1 fixture: indices/distances.npy equal the oracle's
+    faiss search, sw_scores/sw_ids equal the oracle's post_process_sw_static."""
+    fna = os.path.join(GOLDEN, "ecoli_150.fna")
+    fq = os.path.join(GOLDEN, "test_data.fastq")
+    env = dict(os.environ, DRM_BUILD_THREADS="1")
+    r = subprocess.run([os.path.join(ROOT, "bin", "hnswpq_index"), fna, "c1", "150"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(ROOT, "bin", "pipeline"), "c1", fq, fna, "128", "128", "5", "out"],
+                       cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    I = np.load(tmp_path / "out" / "indices.npy")
+    D = np.load(tmp_path / "out" / "distances.npy")
+    assert I.dtype == np.dtype("<u8") and D.dtype == np.dtype("<f4") and I.shape == (150, 128)
+    hdr = open(tmp_path / "out" / "indices.npy", "rb").read(128)
+    assert hdr.startswith(b"\x93NUMPY\x01\x00") and b"{'descr': '<u8', 'fortran_order': False, 'shape': (150, 128), }" in hdr
+    from oracle import faiss_file
+    from deepreadmapper_amd import synth
+    fx = faiss_file.read(str(tmp_path / "c1" / "c1.index"))
+    q = synth.embed(c1["reads"])
+    Do, Io, _, _ = O.hnswpq_search(fx, q, 128, 128)
+    assert np.array_equal(I.astype(np.int64), Io) and np.array_equal(D, Do)
+    from deepreadmapper_amd.rerank import pack_queries
+    qbuf, ql = pack_queries(c1["reads"])
+    rc, sc_o, id_o, cnt_o = O.post_process_sw_static(Io, c1["refs"], 150, qbuf, ql, 1, 128, 128)
+    assert np.array_equal(np.load(tmp_path / "out" / "sw_scores.npy"), sc_o)
+    assert np.array_equal(np.load(tmp_path / "out" / "sw_ids.npy"), id_o)
+    r = subprocess.run([os.path.join(ROOT, "bin", "pipeline"), "nope", fq, fna], cwd=tmp_path,
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and r.stderr.startswith("Error: Config file does not exist")

@@ -1,0 +1,128 @@
+"""CPU tests: the oracle (test infrastructure) pinned against the golden vectors, which were produced
+by the reference's own calc_sw_score and libstdc++ (tests/golden/make_golden.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+
+def _kat():
+    return json.load(open(os.path.join(GOLDEN, "sw_kat.json")))
+
+
+def test_sw_harness_kat():
+    quer = [l.strip() for l in open(os.path.join(GOLDEN, "test_data_quer.txt")).read().splitlines() if l.strip()]
+    kat = _kat()
+    got = [O.calc_sw_score(quer[i].encode(), quer[j].encode()) for i, j in kat["harness_pairs"]]
+    assert got == kat["harness_scores"]
+    assert sum(got) == 2696  # SURVEY.md sec. 8c, measured on the reference build
+
+
+@pytest.mark.parametrize("group", ["edge_cases", "random_pairs"])
+def test_sw_edge_and_random(group):
+    for a, b, s in _kat()[group]:
+        assert O.calc_sw_score(a.encode(), b.encode()) == s, (a, b)
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_vs_reference_build_random():
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        a = bytes(rng.choice(list(b"ACGTN"), size=int(rng.integers(0, 170))).astype(np.uint8))
+        b = bytes(rng.choice(list(b"ACGT<>"), size=int(rng.integers(0, 170))).astype(np.uint8))
+        assert O.calc_sw_score(a, b) == O.ref_calc_sw_score(a, b)
+
+
+def test_c1_score_matrix_sample():
+    mat = np.load(os.path.join(GOLDEN, "sw_c1_matrix.npy"))
+    ref = [l.strip() for l in open(os.path.join(GOLDEN, "test_data_ref.txt"), "rb") if l.strip()]
+    from conftest import read_fastq_tagged
+    reads = read_fastq_tagged(os.path.join(GOLDEN, "test_data.fastq"))
+    assert mat.shape == (len(reads), len(ref)) == (150, 1702)
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        i, j = int(rng.integers(150)), int(rng.integers(1702))
+        assert O.calc_sw_score(ref[j], reads[i]) == mat[i, j]
+    # read _281_1_1_... -> window 561 score 138; read _17_1_1_... -> id 33 score 150
+    lines = open(os.path.join(GOLDEN, "test_data.fastq"), "rb").read().split(b"\n")
+    names = [lines[i] for i in range(0, len(lines) - 1, 4)]
+    i281 = [k for k, n in enumerate(names) if n.startswith(b"@_281_1_1_")][0]
+    i17 = [k for k, n in enumerate(names) if n.startswith(b"@_17_1_1_")][0]
+    assert mat[i281].max() == 138 and int(np.argmax(mat[i281])) == 561
+    assert mat[i17].max() == 150 and int(np.argmax(mat[i17])) == 33
+
+
+def test_partial_sort_matches_libstdcxx():
+    for c in json.load(open(os.path.join(GOLDEN, "partial_sort.json"))):
+        s = np.array(c["scores"], dtype=np.int32)
+        assert O.partial_sort_desc(s, c["k"]).tolist() == c["order"]
+        assert O.stl_partial_sort_desc(s, c["k"]).tolist() == c["order"]
+
+
+def test_windows_reproduce_reference_lookup_table():
+    from deepreadmapper_amd import synth
+    fna = open(os.path.join(GOLDEN, "ecoli_150.fna"), "rb").read().split(b"\n")
+    g = np.frombuffer(b"".join(l.strip() for l in fna[1:]).upper(), dtype=np.uint8)
+    w = synth.windows_lookup(g, 150, 1)
+    ref = [l.strip() for l in open(os.path.join(GOLDEN, "test_data_ref.txt"), "rb") if l.strip()]
+    assert len(w) == len(ref) == 1702
+    assert all(bytes(w[i]) == ref[i] for i in range(len(ref)))
+
+
+def test_post_process_dense_matches_golden_matrix():
+    """oracle post_process_sw_static on all 1702 windows vs the reference-built score matrix."""
+    mat = np.load(os.path.join(GOLDEN, "sw_c1_matrix.npy")).astype(np.int32)
+    ref = np.frombuffer(b"".join(l.strip() for l in open(os.path.join(GOLDEN, "test_data_ref.txt"), "rb")
+                                 if l.strip()), dtype=np.uint8).reshape(1702, 150)
+    from conftest import read_fastq_tagged
+    reads = read_fastq_tagged(os.path.join(GOLDEN, "test_data.fastq"))[:20]
+    qbuf = np.zeros((20, 152), dtype=np.uint8)
+    for i, r in enumerate(reads):
+        qbuf[i, :len(r)] = np.frombuffer(r, dtype=np.uint8)
+    ql = np.array([len(r) for r in reads], dtype=np.int32)
+    nb = np.tile(np.arange(1702, dtype=np.int64), (20, 1))
+    rc, sc, ids, cnt = O.post_process_sw_static(nb, ref, 150, qbuf, ql, 1, 128, 1702)
+    assert rc == 0 and (cnt == 128).all()
+    for i in range(20):
+        order = O.stl_partial_sort_desc(mat[i], 128)
+        assert ids[i].tolist() == order.tolist()
+        assert sc[i].tolist() == mat[i][order].tolist()
+
+
+def test_post_process_errors():
+    ref = np.zeros((10, 16), dtype=np.uint8) + ord("A")
+    q = np.full((1, 8), ord("A"), dtype=np.uint8)
+    ql = np.array([8], dtype=np.int32)
+    rc, *_ = O.post_process_sw_static(np.arange(4, dtype=np.int64)[None], ref, 16, q, ql, 1, 9, 4)
+    assert rc == -1000000000  # k > k_clusters*2*stride
+    nb = np.array([[0, 1, -1, 2]], dtype=np.int64)
+    rc, *_ = O.post_process_sw_static(nb, ref, 16, q, ql, 1, 4, 4)
+    assert rc == -1  # 3 candidates < k = 4 -> "Not enough candidates"
+    rc, sc, ids, cnt = O.post_process_sw_static(np.full((1, 4), -1, np.int64), ref, 16, q, ql, 1, 4, 4)
+    assert rc == 0 and cnt[0] == 0  # no candidate at all: empty result, no throw
+
+
+def test_oracle_exhaustive_search_equals_bruteforce(c1):
+    """ef >= ntotal: the level-0 search visits the whole connected graph, so distances equal the
+    brute-force ADC top-k and ids agree outside the tie group at the k-th distance."""
+    fx = c1["fx"]
+    q = c1["q"][:30]
+    D, I, nd, nh = O.hnswpq_search(fx, q, 50, 4096)
+    cent = fx.centroids.reshape(fx.pq_M, 256, -1)
+    codes = fx.codes.reshape(fx.ntotal, -1)
+    s = O.make_index(fx)
+    for i in range(len(q)):
+        lut = O.pq_distance_table(s, q[i])
+        dist = np.zeros(fx.ntotal, dtype=np.float32)
+        for m in range(fx.pq_M):  # same sequential fp32 order as the restatement
+            dist = (dist + lut[m][codes[:, m]]).astype(np.float32)
+        order = np.lexsort((np.arange(fx.ntotal), dist))[:50]
+        assert np.array_equal(D[i], dist[order])
+        strict = dist[order] < dist[order][-1]
+        assert np.array_equal(I[i][strict], order[strict])
+        assert set(I[i][~strict]) <= set(np.nonzero(dist == dist[order][-1])[0])
+    assert cent.shape[2] == 16

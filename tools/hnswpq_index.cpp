@@ -1,0 +1,98 @@
+// tools/hnswpq_index.cpp -- drop-in for the reference `hnswpq_index` executable
+// (src/hnswpq/index.cpp:195-316). Same argv contract (:197-206):
+//   hnswpq_index <ref_seq.fna|.txt|.npy> <index_prefix> <ref_len> [stride M_pq nbits M_hnsw EFC]
+// Writes <index_prefix>/config.txt (keys of :289-302, save_config) and
+// <index_prefix>/<index_prefix>.index (:212) in faiss IndexHNSWPQ format.
+// Sequence inputs are read as tagged windows (read_file(ref, ref_len, stride), :270) and embedded
+// with the deterministic 3-mer stand-in (OpenVINO is out of scope). Extra knobs via env:
+// DRM_BUILD_THREADS (default: all cores), DRM_BUILD_SEED (default 0).
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <iostream>
+
+#include "drm_hip.h"
+#include "drm_internal.h"
+
+int main(int argc, char *argv[])
+{
+    if (argc < 4 || argc > 9) {
+        std::cerr << "Usage: " << argv[0] << " <ref_seq.txt> <index_prefix> <ref_len> [stride] [M_pq] [nbits] [M_hnsw] [EFC]"
+                  << std::endl;
+        std::cerr << "  stride: step size for sliding window (default: 1)" << std::endl;
+        std::cerr << "  M_pq: number of PQ subquantizers (default: 8)" << std::endl;
+        std::cerr << "  nbits: bits per subquantizer (default: 8)" << std::endl;
+        std::cerr << "  M_hnsw: HNSW connectivity (default: 16)" << std::endl;
+        std::cerr << "  EFC: efConstruction parameter (default: 200)" << std::endl;
+        return 1;
+    }
+    try {
+        const std::string ref_file = argv[1];
+        const std::string prefix = argv[2];
+        const std::string index_file = prefix + "/" + prefix + ".index";
+        const size_t ref_len = std::stoul(argv[3]);
+        const size_t stride = argc >= 5 ? std::stoul(argv[4]) : 1;
+        const int M_pq = argc >= 6 ? std::stoi(argv[5]) : 8;
+        const int nbits = argc >= 7 ? std::stoi(argv[6]) : 8;
+        const int M_hnsw = argc >= 8 ? std::stoi(argv[7]) : 16;
+        const int EFC = argc >= 9 ? std::stoi(argv[8]) : 200;
+        const int threads = std::getenv("DRM_BUILD_THREADS") ? std::atoi(std::getenv("DRM_BUILD_THREADS")) : 0;
+        const uint64_t seed = std::getenv("DRM_BUILD_SEED") ? std::strtoull(std::getenv("DRM_BUILD_SEED"), 0, 10) : 0;
+
+        std::vector<float> emb;
+        size_t n = 0, dim = 128;
+        if (std::filesystem::path(ref_file).extension() == ".npy") {
+            drm::NpyArray a = drm::npy_load(ref_file);
+            if (a.shape.size() != 2) {
+                std::cerr << "Error: Expected 2D array in .npy file" << std::endl;
+                return 1;
+            }
+            if (a.kind != 'f' || a.itemsize != 4)
+                throw drm::Error(DRM_ERR_FORMAT, "embeddings .npy must be float32 ('<f4')");
+            n = a.shape[0];
+            dim = a.shape[1];
+            emb.resize(n * dim);
+            std::memcpy(emb.data(), a.bytes.data(), emb.size() * sizeof(float));
+        } else {
+            std::vector<std::string> seqs, ids;
+            drm::read_file(ref_file, seqs, ids, ref_len, stride, false);
+            if (seqs.empty()) {
+                std::cerr << "No sequences found in file: " << ref_file << std::endl;
+                return 1;
+            }
+            n = seqs.size();
+            std::string all;
+            std::vector<int64_t> off(n);
+            std::vector<int32_t> len(n);
+            for (size_t i = 0; i < n; ++i) {
+                off[i] = (int64_t)all.size();
+                len[i] = (int32_t)seqs[i].size();
+                all += seqs[i];
+            }
+            emb.resize(n * dim);
+            drm::embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)n, (int)dim,
+                             drm::kEmbedSeed, emb.data());
+        }
+        std::cout << "[BUILD INDEX] " << n << " vectors of dimension " << dim << std::endl;
+        std::unordered_map<std::string, drm::ConfigValue> config = {
+            {"index_type", std::string("HNSWPQ")},
+            {"stride", stride},
+            {"ref_len", ref_len},
+            {"n_vects", n},
+            {"dim", dim},
+            {"M_hnsw", (size_t)M_hnsw},
+            {"EFC", (size_t)EFC},
+            {"M_pq", (size_t)M_pq},
+            {"nbits", (size_t)nbits},
+            {"index_file", index_file},
+        };
+        drm::save_config(config, prefix);
+        std::filesystem::create_directories(prefix);
+        drm::build_hnswpq(emb.data(), (int64_t)n, (int)dim, M_pq, nbits, M_hnsw, EFC, 0.5, threads, seed, index_file);
+        std::cout << "[BUILD INDEX] IndexHNSWPQ written to " << index_file << std::endl;
+    } catch (const std::exception &e) {
+        std::cerr << "Error: " << e.what() << std::endl;
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,211 @@
+// tools/pipeline.cpp -- MI355X drop-in for the reference `pipeline` executable (src/main.cpp).
+//
+// Same argv contract (src/main.cpp:12-22):
+//   pipeline <index_prefix> <query_seqs.fastq|.fq|.txt|.npy> <ref_seqs.fasta> [EF] [K] [K_clusters]
+//            [output_dir] [use_dynamic] [use_streaming]
+// Same files: <prefix>/<basename(prefix)>.index + <prefix>/config.txt in (:34-47), and
+// <output_dir>/indices.npy (<u8) + distances.npy (<f4) out (:371-384), written from the raw
+// HNSW results exactly like save_results. The north-star tail (SW rerank, the commented-out
+// post_process_sw_static call at :333-341) runs on the GPU when query sequences are available and
+// adds sw_scores.npy (<i4) and sw_ids.npy (<u8) [n, k] (rows of a query with no candidate: -1 / 2^64-1).
+// Differences, all documented in DESIGN.md: sequence inputs are embedded with the deterministic
+// 3-mer stand-in (the OpenVINO model is out of scope); use_dynamic / use_streaming (SAM streaming)
+// are not implemented (out of scope) and are rejected with an error instead of silently ignored.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <iostream>
+#include <numeric>
+
+#include "drm_hip.h"
+#include "drm_internal.h"
+
+using clk = std::chrono::high_resolution_clock;
+static long ms_since(clk::time_point t0)
+{
+    return (long)std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - t0).count();
+}
+
+static void check(int rc)
+{
+    if (rc != DRM_OK)
+        throw drm::Error(rc, drm_last_error());
+}
+
+int main(int argc, char *argv[])
+{
+    if (argc < 4 || argc > 10) {
+        std::cerr << "Usage: " << argv[0]
+                  << " <index_prefix> <query_seqs.fastq> <ref_seqs.fasta> [EF] [K] [K_clusters] [output_dir] "
+                     "[use_dynamic] [use_streaming]"
+                  << std::endl;
+        std::cerr << "  - query input: Can be FASTQ/FASTA/TXT file or pre-computed embeddings in .npy format" << std::endl;
+        std::cerr << "  - EF: Optional HNSW search parameter (default: 128)" << std::endl;
+        std::cerr << "  - K: Optional number of nearest neighbors to return (default: 128)" << std::endl;
+        std::cerr << "  - output_dir: Optional output directory (default: current directory)" << std::endl;
+        return 1;
+    }
+    try {
+        auto master = clk::now();
+        std::cout << "=== DeepReadMapper MI355X Pipeline ===" << std::endl << std::endl;
+        const std::string prefix = argv[1];
+        const std::string base = std::filesystem::path(prefix).filename().string();
+        const std::string index_file = prefix + "/" + base + ".index";
+        const std::string config_file = prefix + "/config.txt";
+        if (!std::filesystem::exists(config_file))
+            throw drm::Error(DRM_ERR_IO, "Config file does not exist: " + config_file);
+        auto config = drm::load_config(config_file);
+        if (!config.count("ref_len") || !std::holds_alternative<size_t>(config["ref_len"]) || !config.count("stride") ||
+            !std::holds_alternative<size_t>(config["stride"]))
+            throw drm::Error(DRM_ERR_FORMAT, "config.txt lacks integer ref_len / stride");
+        const size_t ref_len = std::get<size_t>(config["ref_len"]);
+        const size_t stride = std::get<size_t>(config["stride"]);
+        const std::string query_file = argv[2], ref_file = argv[3];
+        const int ef = argc >= 5 ? std::stoi(argv[4]) : 128;
+        const int k = argc >= 6 ? std::stoi(argv[5]) : 128;
+        int k_clusters = 5;
+        if (stride == 1)
+            k_clusters = k;
+        else if (argc >= 7)
+            k_clusters = std::stoi(argv[6]);
+        const std::string out_dir = argc >= 8 ? argv[7] : ".";
+        const bool use_dynamic = argc >= 9 && std::stoi(argv[8]) != 0;
+        const bool use_streaming = argc >= 10 && std::stoi(argv[9]) != 0;
+        if (use_dynamic || use_streaming)
+            throw drm::Error(DRM_ERR_UNSUPPORTED, "use_dynamic / use_streaming are not supported by this build");
+        int device = 0;
+        if (const char *dv = std::getenv("DRM_DEVICE"))
+            device = std::atoi(dv);
+
+        // ---- data loading
+        std::vector<float> emb;
+        size_t nq = 0, dim = 0;
+        std::vector<std::string> qseqs, qids;
+        const bool is_npy = std::filesystem::path(query_file).extension() == ".npy";
+        auto t0 = clk::now();
+        if (is_npy) {
+            drm::NpyArray a = drm::npy_load(query_file);
+            if (a.shape.size() != 2)
+                throw drm::Error(DRM_ERR_FORMAT, "Error: Expected 2D array in .npy file");
+            if (a.kind != 'f' || a.itemsize != 4)
+                throw drm::Error(DRM_ERR_FORMAT, "embeddings .npy must be float32 ('<f4')");
+            nq = a.shape[0];
+            dim = a.shape[1];
+            emb.resize(nq * dim);
+            std::memcpy(emb.data(), a.bytes.data(), emb.size() * sizeof(float));
+            std::cout << "[MAIN] Loaded " << nq << " embeddings of dimension " << dim << std::endl;
+        } else {
+            drm::read_file(query_file, qseqs, qids);
+            if (qseqs.empty()) {
+                std::cerr << "No query_sequences found in input file!" << std::endl;
+                return 1;
+            }
+            nq = qseqs.size();
+        }
+        std::vector<std::string> refs;
+        if (!is_npy) {
+            std::vector<std::string> dummy;
+            drm::read_file(ref_file, refs, dummy, ref_len, 1, true);
+            std::cout << "[MAIN] Loaded " << refs.size() << " reference sequences from " << ref_file << std::endl;
+        }
+        std::cout << "[MAIN] Total Data loading time: " << ms_since(t0) << " ms" << std::endl << std::endl;
+
+        // ---- index
+        t0 = clk::now();
+        if (!std::filesystem::exists(index_file))
+            throw drm::Error(DRM_ERR_IO, "Index file does not exist: " + index_file);
+        drm_index *index = nullptr;
+        check(drm_index_load(index_file.c_str(), device, &index));
+        drm_index_info info;
+        check(drm_index_get_info(index, &info));
+        std::cout << "[MAIN] Index loaded time: " << ms_since(t0) << " ms (" << info.ntotal << " vectors, "
+                  << info.device_bytes / (1 << 20) << " MiB on device " << device << ")" << std::endl;
+
+        // ---- embedding (stand-in for the OpenVINO model)
+        if (!is_npy) {
+            t0 = clk::now();
+            dim = (size_t)info.d;
+            std::string all;
+            std::vector<int64_t> off(nq);
+            std::vector<int32_t> len(nq);
+            for (size_t i = 0; i < nq; ++i) {
+                off[i] = (int64_t)all.size();
+                len[i] = (int32_t)qseqs[i].size();
+                all += qseqs[i];
+            }
+            emb.resize(nq * dim);
+            check(drm_embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)nq, (int32_t)dim,
+                                  drm::kEmbedSeed, emb.data()));
+            std::cout << "[MAIN] Inference (3-mer stand-in) time: " << ms_since(t0) << " ms" << std::endl;
+        }
+
+        // ---- HNSW search (faiss_search(alg_hnsw, embeddings, k_clusters, ef), src/main.cpp:278)
+        t0 = clk::now();
+        std::vector<float> D(nq * (size_t)k_clusters);
+        std::vector<int64_t> I(nq * (size_t)k_clusters);
+        drm_search_stats st{};
+        check(drm_search(index, emb.data(), (int64_t)nq, (int32_t)dim, k_clusters, ef, D.data(), I.data(), &st));
+        std::cout << "[MAIN] Search time: " << ms_since(t0) << " ms (kernel " << st.kernel_ms << " ms, ndis "
+                  << st.ndis << ", nhops " << st.nhops << ")" << std::endl;
+        check(drm_index_free(index));
+
+        // ---- SW rerank (post_process_sw_static)
+        std::vector<int32_t> sw_scores;
+        std::vector<uint64_t> sw_ids;
+        if (!is_npy) {
+            t0 = clk::now();
+            drm_refs *rt = nullptr;
+            std::string table(refs.size() * ref_len, '\0');
+            for (size_t r = 0; r < refs.size(); ++r)
+                std::memcpy(&table[r * ref_len], refs[r].data(), ref_len);
+            check(drm_refs_create((const uint8_t *)table.data(), (int64_t)refs.size(), (int32_t)ref_len,
+                                  (int64_t)ref_len, device, &rt));
+            size_t qs = 0;
+            for (auto &q : qseqs)
+                qs = std::max(qs, q.size());
+            std::string qbuf(nq * qs, '\0');
+            std::vector<int32_t> ql(nq);
+            for (size_t i = 0; i < nq; ++i) {
+                std::memcpy(&qbuf[i * qs], qseqs[i].data(), qseqs[i].size());
+                ql[i] = (int32_t)qseqs[i].size();
+            }
+            sw_scores.assign(nq * (size_t)k, -1);
+            sw_ids.assign(nq * (size_t)k, ~0ull);
+            std::vector<int32_t> counts(nq);
+            int64_t bad = -1;
+            int rc = drm_post_process_sw_static(rt, I.data(), (int64_t)nq, k_clusters, (const uint8_t *)qbuf.data(),
+                                                ql.data(), (int32_t)qs, (int64_t)stride, k, k_clusters,
+                                                sw_scores.data(), sw_ids.data(), counts.data(), &bad);
+            drm_refs_free(rt);
+            check(rc);
+            std::cout << "[MAIN] Post-processing (SW rerank) time: " << ms_since(t0) << " ms" << std::endl;
+        }
+
+        // ---- outputs (save_results, src/utils/utils.cpp:264-334)
+        t0 = clk::now();
+        std::filesystem::create_directories(out_dir);
+        const size_t kout = stride == 1 ? (size_t)k : (size_t)k_clusters;
+        std::vector<uint64_t> idx(nq * kout);
+        std::vector<float> dis(nq * kout);
+        for (size_t i = 0; i < nq; ++i)
+            for (size_t j = 0; j < kout; ++j) {
+                idx[i * kout + j] = (uint64_t)I[i * k_clusters + j];
+                dis[i * kout + j] = D[i * k_clusters + j];
+            }
+        drm::npy_save(out_dir + "/indices.npy", idx.data(), {nq, kout}, 'u', 8);
+        drm::npy_save(out_dir + "/distances.npy", dis.data(), {nq, kout}, 'f', 4);
+        if (!sw_scores.empty()) {
+            drm::npy_save(out_dir + "/sw_scores.npy", sw_scores.data(), {nq, (size_t)k}, 'i', 4);
+            drm::npy_save(out_dir + "/sw_ids.npy", sw_ids.data(), {nq, (size_t)k}, 'u', 8);
+        }
+        std::cout << "[MAIN] Output saving time: " << ms_since(t0) << " ms" << std::endl;
+        std::cout << "[MAIN] Total pipeline time: " << ms_since(master) << " ms" << std::endl;
+        std::cout << "=== Pipeline Completed Successfully! ===" << std::endl;
+    } catch (const std::exception &e) {
+        std::cerr << "Error: " << e.what() << std::endl;
+        return 1;
+    }
+    return 0;
+}
