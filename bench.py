@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""bench.py -- mapped reads/s of the MI355X hot path (HNSW-PQ search + SW rerank, EF=128, K=128).
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
+torch.distributed.run, one rank per GPU. One step = one pass of the hot path over this rank's batch
+of synthetic 150 bp reads, inputs already resident in HBM: the HNSW-PQ search kernel
+(faiss_search(index, emb, k_clusters=K, ef=EF), src/main.cpp:278) followed by the SW rerank kernel
+(post_process_sw_static(..., k=K, k_clusters=K), src/main.cpp:340). Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json configs[2] "C3"): a seeded 500,149 bp genome, stride-1
+dense index of 1,000,000 fwd/RC 150 bp windows (IndexHNSWPQ M_pq=8 nbits=8 M_hnsw=16 EFC=200, built
+here since faiss is absent), 100,000 reads per GPU (1 % substitutions; weak scaling: the per-GPU batch
+is fixed). Queries are embedded with the 3-mer stand-in (the OpenVINO encoder is out of scope); the
+reference's timed "Search time" window likewise excludes inference (src/main.cpp:272-285).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Dist:
+    """Control plane for N>1 ranks (barrier, max, sum) over torch.distributed gloo; the data path
+    has no collective (queries are independent, the index is replicated per GPU)."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist  # imported before libdrm_hip.so is loaded
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def allreduce(self, v, op):
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn):
+    """Oracle (C restatement, OpenMP over queries) on a bounded sample of this workload."""
+    from oracle import faiss_file, oracle as O
+    from deepreadmapper_amd.rerank import pack_queries
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    fx = faiss_file.read(index_path)
+    s = O.make_index(fx)
+    refs = w.refs
+
+    def run(n):
+        q = q_emb[:n]
+        t0 = time.perf_counter()
+        D, I, nd, nh = O.hnswpq_search(s, q, k, ef, nthreads=threads)
+        t1 = time.perf_counter()
+        qbuf, ql = queries[:n], np.full(n, queries.shape[1], dtype=np.int32)
+        rc, sc, ids, cnt = O.post_process_sw_static(I, refs, refs.shape[1], qbuf, ql, 1, k, k, nthreads=threads)
+        t2 = time.perf_counter()
+        return t1 - t0, t2 - t1
+
+    ts, tw = run(min(256, len(q_emb)))
+    per_q = (ts + tw) / min(256, len(q_emb))
+    n = int(max(256, min(len(q_emb), budget_s / max(per_q, 1e-6))))
+    ts, tw = run(n)
+    log_fn(f"[cpu] oracle on {n} queries x {threads} threads: search {ts:.2f}s, SW {tw:.2f}s")
+    return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} of this rank's C3 reads (oracle/ C restatement, OpenMP {threads} threads): "
+                      f"search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--queries", type=int, default=100_000, help="reads per GPU (weak scaling)")
+    ap.add_argument("--ef", type=int, default=128)
+    ap.add_argument("--k", type=int, default=128)
+    ap.add_argument("--cache", default=os.environ.get("DRM_BENCH_CACHE", "/tmp/drm_bench_cache"))
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--build-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    D = Dist()
+    from deepreadmapper_amd import synth
+    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream, set_device, synchronize
+    from deepreadmapper_amd.search import HnswPqIndex
+    from deepreadmapper_amd.rerank import WindowTable
+    from deepreadmapper_amd._native import check, lib
+
+    set_device(D.local_rank)
+    N, Q, K, EF = D.world, args.queries, args.k, args.ef
+    w = synth.Workload("c3", 500_149, N * Q, seed=42, read_seed=7)
+    # rank 0 builds the shared index file; the others wait, then every rank loads its own replica
+    if D.rank == 0:
+        t0 = time.time()
+        w.generate(args.cache, nthreads=args.build_threads, log=log)
+        log(f"[bench] workload ready in {time.time() - t0:.1f}s: {len(w.refs)} windows, index {w.index_path}")
+    D.barrier()
+    if D.rank != 0:
+        w.generate(args.cache)
+    lo, hi = D.rank * Q, (D.rank + 1) * Q
+    q_emb = np.ascontiguousarray(w.q_emb[lo:hi])
+    queries = np.ascontiguousarray(w.queries[lo:hi])
+    truth = w.truth[lo:hi]
+
+    ix = HnswPqIndex(w.index_path, D.local_rank)
+    table = WindowTable(w.refs, D.local_rank)
+    d_x = DeviceBuffer.from_host(q_emb)
+    d_q = DeviceBuffer.from_host(queries)
+    d_ql = DeviceBuffer.from_host(np.full(Q, queries.shape[1], dtype=np.int32))
+    d_D = DeviceBuffer((Q, K), np.float32)
+    d_I = DeviceBuffer((Q, K), np.int64)
+    d_nd, d_nh, d_nu = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
+    d_sc, d_id, d_st = DeviceBuffer((Q, K), np.int32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
+    stream = Stream()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        ix.search_device(d_x, Q, K, EF, d_D, d_I, d_nd, d_nh, stream, d_nhops_upper=d_nu)
+        if ev:
+            ev[1].record(stream)
+        check(lib().drm_post_process_sw_static_device(table.handle, d_I.ptr, Q, K, d_q.ptr, d_ql.ptr,
+                                                      queries.shape[1], 1, K, K, d_sc.ptr, d_id.ptr, d_st.ptr,
+                                                      stream.handle))
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    events = [[Event(), Event(), Event()] for _ in range(args.steps)]
+    D.barrier()
+    synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(events[s])
+    stream.synchronize()
+    synchronize()
+    elapsed = time.perf_counter() - t0
+    D.barrier()
+    elapsed_max = D.allreduce(elapsed, "MAX")
+    search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
+    sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
+
+    # correctness / quality of this rank's last step
+    st = d_st.download()
+    if not (st == K).all():
+        raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")
+    ndis, nhops, nup = d_nd.download().astype(np.int64), d_nh.download().astype(np.int64), d_nu.download()
+    ids = d_id.download()
+    top1 = float(np.mean(ids[:, 0].astype(np.int64) == truth))
+    intop = float(np.mean((ids.astype(np.int64) == truth[:, None]).any(axis=1)))
+
+    # algorithmic bytes of the search kernel, per launch:
+    #   512 (query) + 2*M*4 per level-0 hop + M*4 per upper hop + ndis*code_size + K*12 (ids+dists)
+    info = ix.info
+    deg0 = 2 * info.M_hnsw
+    code = (info.pq_M * info.pq_nbits + 7) // 8
+    l0 = nhops - nup
+    bytes_q = 4 * info.d + l0 * deg0 * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
+    codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
+    bytes_launch = float(bytes_q.sum() + codebook)
+    achieved = bytes_launch / (search_ms * 1e-3) / 1e9
+    cells = float(Q) * K * w.refs.shape[1] * queries.shape[1]
+
+    total_reads = float(N * Q * args.steps)
+    value = total_reads / elapsed_max
+    result = None
+    if D.rank == 0:
+        cpu = None
+        if N == 1 and not args.no_cpu:
+            cpu = cpu_baseline(w, w.index_path, queries, q_emb, K, EF, args.cpu_budget, log)
+        result = {
+            "metric": "mapped reads/sec, 150 bp queries, EF=128 K=128",
+            "value": round(value, 1), "unit": "reads/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32 (PQ-ADC distances) + int32 (SW DP)",
+            "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
+            "config": {"workload": "C3: synthetic 1M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 "
+                                   "EFC=200), search + SW rerank, EF=128 K=128",
+                       "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
+                       "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
+            "roofline": {"bound": "hbm", "kernel": "hnsw_pq_search_kernel", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None, "bytes_per_launch": bytes_launch,
+                         "avg_launch_ms": round(search_ms, 4)},
+            "cpu_baseline": cpu,
+            "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
+                          "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
+                          "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
+                          "bytes_per_query": round(float(bytes_q.mean()), 1),
+                          "truth_top1": round(top1, 4), "truth_in_topk": round(intop, 4)},
+        }
+        print(json.dumps(result), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

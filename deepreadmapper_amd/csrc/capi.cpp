@@ -273,6 +273,12 @@ int drm_index_get_info(const drm_index *index, drm_index_info *info)
 int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                       int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, void *stream)
 {
+    return drm_search_device_ex(index, d_x, n, k, ef, d_D, d_I, d_ndis, d_nhops, nullptr, stream);
+}
+
+int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                         int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, void *stream)
+{
     return guarded([&] {
         if (!index)
             throw Error(DRM_ERR_ARG, "null index");
@@ -290,7 +296,7 @@ int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, 
             if (!nh)
                 nh = tmp->p + n;
         }
-        drm::launch_hnsw_search(index->dev, d_x, n, k, ef, d_D, d_I, nd, nh, (hipStream_t)stream);
+        drm::launch_hnsw_search(index->dev, d_x, n, k, ef, d_D, d_I, nd, nh, d_nhops_upper, (hipStream_t)stream);
         if (tmp)
             DRM_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
     });
@@ -318,7 +324,7 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
         DRM_HIP_CHECK(hipEventCreate(&e0));
         DRM_HIP_CHECK(hipEventCreate(&e1));
         DRM_HIP_CHECK(hipEventRecord(e0, nullptr));
-        drm::launch_hnsw_search(index->dev, dx.p, n, k, ef, dD.p, dI.p, dst.p, dst.p + n, nullptr);
+        drm::launch_hnsw_search(index->dev, dx.p, n, k, ef, dD.p, dI.p, dst.p, dst.p + n, nullptr, nullptr);
         DRM_HIP_CHECK(hipEventRecord(e1, nullptr));
         DRM_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0.f;
@@ -404,8 +410,10 @@ int drm_refs_free(drm_refs *refs)
         if (!refs)
             return;
         (void)hipSetDevice(refs->dev.device);
-        if (refs->dev.windows)
-            (void)hipFree(refs->dev.windows);
+        for (void *p : {(void *)refs->dev.windows, (void *)refs->dev.ws_ids, (void *)refs->dev.ws_scores,
+                        (void *)refs->dev.ws_ncand})
+            if (p)
+                (void)hipFree(p);
         delete refs;
     });
 }

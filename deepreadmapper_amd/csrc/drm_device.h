@@ -62,6 +62,7 @@ struct SearchArgs {
     int64_t *I;
     int32_t *ndis;
     int32_t *nhops;
+    int32_t *nhops_upper; // optional: greedy hops on levels >= 1 (for the bytes model)
     uint32_t *visited;
     int64_t vis_words;
     int32_t *clear_list;
@@ -71,7 +72,7 @@ struct SearchArgs {
 };
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
-                        int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream);
+                        int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------- SW rerank
 struct DeviceRefs {
@@ -80,6 +81,11 @@ struct DeviceRefs {
     int64_t n_ref = 0;
     int32_t ref_len = 0;
     int64_t row_stride = 0;
+    // rerank workspace (grown on demand): candidate ids / SW scores / candidate counts per query
+    uint64_t *ws_ids = nullptr;
+    int32_t *ws_scores = nullptr;
+    int32_t *ws_ncand = nullptr;
+    size_t ws_elems = 0, ws_nq = 0;
 };
 
 struct RerankArgs {
@@ -98,11 +104,16 @@ struct RerankArgs {
     int32_t *top_scores;
     uint64_t *top_ids;
     int32_t *status;
+    // workspace (set by launch_sw_rerank)
+    int32_t cmax;
+    uint64_t *cand_ids;
+    int32_t *cand_scores;
+    int32_t *ncand;
 };
 
 constexpr int kMaxCands = 1024; // candidates per query kept in LDS
 
-void launch_sw_rerank(const DeviceRefs &refs, const RerankArgs &a, int max_qlen, hipStream_t stream);
+void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t stream);
 
 // generic batched calc_sw_score: one wave per pair
 void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *d_len1, const uint8_t *d_s2,

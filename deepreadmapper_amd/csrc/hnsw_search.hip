@@ -202,6 +202,8 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             if (lane == 0) {
                 a.ndis[q] = 0;
                 a.nhops[q] = 0;
+                if (a.nhops_upper)
+                    a.nhops_upper[q] = 0;
             }
             continue;
         }
@@ -401,6 +403,8 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
         if (lane == 0) {
             a.ndis[q] = ndis + ndis0;
             a.nhops[q] = nhops + nstep;
+            if (a.nhops_upper)
+                a.nhops_upper[q] = nhops;
         }
 
         // --- VisitedTable::advance: clear exactly the bits this query set
@@ -419,7 +423,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
 } // namespace
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
-                        int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream)
+                        int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream)
 {
     if (n <= 0)
         return;
@@ -498,6 +502,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.I = d_I;
     a.ndis = d_ndis;
     a.nhops = d_nhops;
+    a.nhops_upper = d_nhops_upper;
     a.visited = ix.visited;
     a.vis_words = ix.vis_words;
     a.clear_list = ix.clear_list;

@@ -28,16 +28,20 @@ constexpr int kPadRow = 256; // profile row index for "matches nothing"
 
 // One DP row update for the full register row H[0..LQ).
 template <int LQ>
-__device__ __forceinline__ void sw_row(int (&H)[LQ], const uint32_t (&bv)[LQ / 16], int &best)
+__device__ __forceinline__ void sw_row(int (&H)[LQ], const uint32_t (&bv)[(LQ + 15) / 16], int &best)
 {
-    int diag = 0, left = 0;
+    // The next cell's diagonal term (old H[j] + 2*match) is formed before H[j] is overwritten, so the
+    // old and new H[j] never overlap and stay in one register (no per-cell v_mov).
+    int t_next = (int)__builtin_amdgcn_ubfe(bv[0], 0u, 2u); // diag of column 0 is the zero border
+    int left = 0;
 #pragma unroll
     for (int j = 0; j < LQ; ++j) {
-        const uint32_t m2 = (bv[j >> 4] >> (2 * (j & 15))) & 2u;
+        const int t = t_next;
         const int up = H[j];
-        int h = max(max((int)(diag + (int)m2), up), left);
+        if (j + 1 < LQ)
+            t_next = up + (int)__builtin_amdgcn_ubfe(bv[(j + 1) >> 4], 2u * ((j + 1) & 15), 2u); // bit 2t is 0
+        int h = max(max(t, up), left);
         h = max(h - 1, 0);
-        diag = up;
         H[j] = h;
         left = h;
         best = max(best, h);
@@ -45,9 +49,9 @@ __device__ __forceinline__ void sw_row(int (&H)[LQ], const uint32_t (&bv)[LQ / 1
 }
 
 template <int LQ>
-__device__ __forceinline__ void load_profile(const uint32_t *prof, int ch, uint32_t (&bv)[LQ / 16])
+__device__ __forceinline__ void load_profile(const uint32_t *prof, int ch, uint32_t (&bv)[(LQ + 15) / 16])
 {
-    constexpr int NW = LQ / 16;
+    constexpr int NW = (LQ + 15) / 16;
     constexpr int NWP = (NW + 3) & ~3;
     const uint4 *p = reinterpret_cast<const uint4 *>(prof + (size_t)ch * NWP);
 #pragma unroll
@@ -67,7 +71,7 @@ __device__ __forceinline__ void load_profile(const uint32_t *prof, int ch, uint3
 template <int LQ>
 __device__ void build_profile(uint32_t *prof, const uint8_t *q, int qlen)
 {
-    constexpr int NW = LQ / 16;
+    constexpr int NW = (LQ + 15) / 16;
     constexpr int NWP = (NW + 3) & ~3;
     for (int e = threadIdx.x; e < 257 * NWP; e += blockDim.x) {
         const int b = e / NWP, w = e % NWP;
@@ -137,25 +141,40 @@ __device__ void ps_partial_sort(uint32_t *e, int n, int k)
     }
 }
 
+// Kernel 1 of the rerank: candidate lists (find_sequences static) + one SW score per candidate.
+// One 128-thread workgroup per query (grid-stride); lane = candidate.
 template <int LQ>
-__global__ __launch_bounds__(128) void sw_rerank_kernel(RerankArgs a)
+__global__ __launch_bounds__(128) void sw_score_kernel(RerankArgs a)
 {
-    constexpr int NW = LQ / 16;
+    constexpr int NW = (LQ + 15) / 16;
     constexpr int NWP = (NW + 3) & ~3;
     __shared__ __align__(16) uint32_t prof[257 * NWP];
     __shared__ __align__(16) uint8_t qbuf[LQ];
     __shared__ uint64_t cand[kMaxCands];
-    __shared__ uint32_t elem[kMaxCands];
+    __shared__ int wave_cnt[2];
     __shared__ int ncand_s;
 
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
         const int qlen = a.q_len[q];
-        // --- candidate list (find_sequences static): dense keeps ids < n_ref in order; sparse
-        //     expands sparse_id*stride to [pos-stride+1, pos+stride) with duplicates kept.
-        if (tid == 0) {
-            const int nsel = min(a.k_clusters, a.kk);
-            const int64_t *nb = a.neighbors + q * a.kk;
+        const int nsel = min(a.k_clusters, a.kk);
+        const int64_t *nb = a.neighbors + q * a.kk;
+        if (a.stride == 1 && nsel <= 128) {
+            // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
+            const uint64_t id = (tid < nsel) ? (uint64_t)nb[tid] : ~0ull;
+            const bool keep = id < (uint64_t)a.n_ref;
+            const uint64_t m = __ballot(keep);
+            if (lane == 0)
+                wave_cnt[wv] = __popcll(m);
+            __syncthreads();
+            const int base = (wv == 1) ? wave_cnt[0] : 0;
+            if (keep)
+                cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = id;
+            if (tid == 0)
+                ncand_s = wave_cnt[0] + wave_cnt[1];
+        } else if (tid == 0) {
+            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride), duplicates kept
             int nc = 0;
             bool overflow = false;
             for (int i = 0; i < nsel && !overflow; ++i) {
@@ -167,87 +186,92 @@ __global__ __launch_bounds__(128) void sw_rerank_kernel(RerankArgs a)
                         else
                             cand[nc++] = id;
                     }
-                } else {
-                    const uint64_t s = (uint64_t)a.stride;
-                    const uint64_t actual = id * s;
-                    if (actual >= (uint64_t)a.n_ref)
-                        continue;
-                    const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
-                    const uint64_t end = min(actual + s, (uint64_t)a.n_ref);
-                    for (uint64_t pos = start; pos < end; ++pos) {
-                        if (nc >= kMaxCands) {
-                            overflow = true;
-                            break;
-                        }
-                        cand[nc++] = pos;
+                    continue;
+                }
+                const uint64_t s = (uint64_t)a.stride;
+                const uint64_t actual = id * s;
+                if (actual >= (uint64_t)a.n_ref)
+                    continue;
+                const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
+                const uint64_t end = min(actual + s, (uint64_t)a.n_ref);
+                for (uint64_t pos = start; pos < end; ++pos) {
+                    if (nc >= kMaxCands) {
+                        overflow = true;
+                        break;
                     }
+                    cand[nc++] = pos;
                 }
             }
-            ncand_s = overflow ? -1 : nc;
+            ncand_s = overflow ? -2 : nc;
         }
         for (int t = tid; t < LQ; t += blockDim.x)
             qbuf[t] = (t < qlen) ? a.queries[q * a.q_stride + t] : 0;
         __syncthreads();
         build_profile<LQ>(prof, qbuf, qlen);
         __syncthreads();
-        const int ncand = (qlen > LQ) ? -3 : ncand_s; // -3: query longer than this build's LQ
+        const int ncand = (qlen > LQ) ? -3 : ncand_s;
+        if (tid == 0)
+            a.ncand[q] = ncand;
+        for (int c = tid; c < ncand; c += blockDim.x) {
+            int H[LQ];
+#pragma unroll
+            for (int j = 0; j < LQ; ++j)
+                H[j] = 0;
+            int best = 0;
+            const uint64_t wid = cand[c];
+            const uint8_t *win = a.refs + (size_t)wid * (size_t)a.row_stride;
+            const int L = a.ref_len;
+            int ch_next = (L > 0) ? (int)win[0] : kPadRow;
+            for (int i = 0; i < L; ++i) {
+                const int ch = ch_next;
+                if (i + 1 < L)
+                    ch_next = win[i + 1]; // prefetch the next row's byte
+                uint32_t bv[NW];
+                load_profile<LQ>(prof, ch, bv);
+                sw_row<LQ>(H, bv, best);
+            }
+            a.cand_ids[q * a.cmax + c] = wid;
+            a.cand_scores[q * a.cmax + c] = best;
+        }
+        __syncthreads();
+    }
+}
 
-        if (ncand > 0) {
-            // --- SW scores, one lane per candidate
-            for (int c = tid; c < ncand; c += blockDim.x) {
-                int H[LQ];
-#pragma unroll
-                for (int j = 0; j < LQ; ++j)
-                    H[j] = 0;
-                int best = 0;
-                const uint8_t *win = a.refs + (size_t)cand[c] * (size_t)a.row_stride;
-                const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win); // rows are 16-B aligned
-                const int L = a.ref_len;
-                uint32_t nxt = (L > 0) ? w32[0] : 0u;
-                for (int i0 = 0; i0 < L; i0 += 4) {
-                    const uint32_t cur = nxt;
-                    if (i0 + 4 < L)
-                        nxt = w32[(i0 >> 2) + 1]; // prefetch the next 4 candidate bytes
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int ch = (i0 + t < L) ? (int)((cur >> (8 * t)) & 255u) : kPadRow;
-                        uint32_t bv[NW];
-                        load_profile<LQ>(prof, ch, bv);
-                        sw_row<LQ>(H, bv, best);
-                    }
-                }
-                elem[c] = ((uint32_t)best << 16) | (uint32_t)c;
-            }
+// Kernel 2 of the rerank: sw_reranker's std::partial_sort + output, one thread per query. Each
+// thread replays libstdc++'s heap algorithm on its own padded LDS array (stride cmax+1 words, so
+// threads touching the same heap index hit different banks).
+__global__ __launch_bounds__(64) void sw_topk_kernel(RerankArgs a)
+{
+    extern __shared__ uint32_t heap_lds[];
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.nq)
+        return;
+    uint32_t *e = heap_lds + (size_t)threadIdx.x * (size_t)(a.cmax + 1);
+    const int ncand = a.ncand[q];
+    int status;
+    if (ncand < 0)
+        status = ncand; // -2: > kMaxCands candidates, -3: query longer than the SW build
+    else if (ncand == 0 || a.k == 0)
+        status = 0; // reranker.cpp:10-11: empty result for this query
+    else if (ncand < a.k)
+        status = -1; // reranker.cpp:26-29
+    else
+        status = a.k;
+    a.status[q] = status;
+    if (status > 0) {
+        for (int c = 0; c < ncand; ++c)
+            e[c] = ((uint32_t)a.cand_scores[q * a.cmax + c] << 16) | (uint32_t)c;
+        ps_partial_sort(e, ncand, a.k);
+        for (int j = 0; j < a.k; ++j) {
+            const uint32_t v = e[j];
+            a.top_scores[q * a.k + j] = (int32_t)(v >> 16);
+            a.top_ids[q * a.k + j] = a.cand_ids[q * a.cmax + (v & 0xFFFFu)];
         }
-        __syncthreads();
-        // --- sw_reranker ordering + outputs
-        if (tid == 0) {
-            int status;
-            if (ncand < 0)
-                status = ncand == -3 ? -3 : -2; // -2: > kMaxCands candidates, -3: query > LQ bytes
-            else if (ncand == 0 || a.k == 0)
-                status = 0; // reranker.cpp:10-11: empty result for this query
-            else if (ncand < a.k)
-                status = -1; // reranker.cpp:26-29
-            else {
-                ps_partial_sort(elem, ncand, a.k);
-                status = a.k;
-            }
-            a.status[q] = status;
+    } else {
+        for (int j = 0; j < a.k; ++j) {
+            a.top_scores[q * a.k + j] = -1;
+            a.top_ids[q * a.k + j] = ~0ull;
         }
-        __syncthreads();
-        const int st = a.status[q];
-        for (int j = tid; j < a.k; j += blockDim.x) {
-            if (st > 0) {
-                const uint32_t e = elem[j];
-                a.top_scores[q * a.k + j] = (int32_t)(e >> 16);
-                a.top_ids[q * a.k + j] = cand[e & 0xFFFFu];
-            } else {
-                a.top_scores[q * a.k + j] = -1;
-                a.top_ids[q * a.k + j] = ~0ull;
-            }
-        }
-        __syncthreads();
     }
 }
 
@@ -258,7 +282,7 @@ __global__ __launch_bounds__(64) void sw_pairs_kernel(const uint8_t *s1, const i
                                                       const uint8_t *s2, const int64_t *off2, const int32_t *len2,
                                                       int64_t npairs, int32_t *scores)
 {
-    constexpr int NW = LQ / 16;
+    constexpr int NW = (LQ + 15) / 16;
     constexpr int NWP = (NW + 3) & ~3;
     __shared__ __align__(16) uint32_t prof[257 * NWP];
     __shared__ __align__(16) uint8_t qbuf[LQ];
@@ -294,15 +318,15 @@ static int pick_lq(int max_qlen)
 {
     if (max_qlen <= 64)
         return 64;
-    if (max_qlen <= 160)
-        return 160;
+    if (max_qlen <= 152) // 150 bp reads + "<" ">" tags (format_fastq)
+        return 152;
     if (max_qlen <= 256)
         return 256;
     throw Error(DRM_ERR_UNSUPPORTED,
                 "query length " + std::to_string(max_qlen) + " > 256 is not supported by the GPU SW kernel yet");
 }
 
-void launch_sw_rerank(const DeviceRefs &refs, const RerankArgs &a, int max_qlen, hipStream_t stream)
+void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t stream)
 {
     if (a.nq <= 0)
         return;
@@ -310,18 +334,48 @@ void launch_sw_rerank(const DeviceRefs &refs, const RerankArgs &a, int max_qlen,
         throw Error(DRM_ERR_UNSUPPORTED, "k > 1024 not supported by the GPU rerank kernel");
     if (refs.row_stride % 16 != 0)
         throw Error(DRM_ERR_ARG, "window table row stride must be a multiple of 16");
+    const int64_t nsel = std::min(a.k_clusters, a.kk);
+    const int64_t cmax = std::max<int64_t>(1, std::min<int64_t>(kMaxCands, a.stride == 1 ? nsel : nsel * (2 * a.stride - 1)));
+    const size_t need = (size_t)a.nq * (size_t)cmax;
+    if (need > refs.ws_elems || !refs.ws_ncand || (size_t)a.nq > refs.ws_nq) {
+        if (refs.ws_ids)
+            DRM_HIP_CHECK(hipFree(refs.ws_ids));
+        if (refs.ws_scores)
+            DRM_HIP_CHECK(hipFree(refs.ws_scores));
+        if (refs.ws_ncand)
+            DRM_HIP_CHECK(hipFree(refs.ws_ncand));
+        refs.ws_ids = nullptr;
+        refs.ws_scores = nullptr;
+        refs.ws_ncand = nullptr;
+        DRM_HIP_CHECK(hipMalloc(&refs.ws_ids, sizeof(uint64_t) * need));
+        DRM_HIP_CHECK(hipMalloc(&refs.ws_scores, sizeof(int32_t) * need));
+        DRM_HIP_CHECK(hipMalloc(&refs.ws_ncand, sizeof(int32_t) * (size_t)a.nq));
+        refs.ws_elems = need;
+        refs.ws_nq = (size_t)a.nq;
+    }
+    a.cmax = (int32_t)cmax;
+    a.cand_ids = refs.ws_ids;
+    a.cand_scores = refs.ws_scores;
+    a.ncand = refs.ws_ncand;
     const int grid = (int)std::min<int64_t>(a.nq, 65536);
     switch (pick_lq(max_qlen)) {
     case 64:
-        hipLaunchKernelGGL(sw_rerank_kernel<64>, dim3(grid), dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(sw_score_kernel<64>, dim3(grid), dim3(128), 0, stream, a);
         break;
-    case 160:
-        hipLaunchKernelGGL(sw_rerank_kernel<160>, dim3(grid), dim3(128), 0, stream, a);
+    case 152:
+        hipLaunchKernelGGL(sw_score_kernel<152>, dim3(grid), dim3(128), 0, stream, a);
         break;
     default:
-        hipLaunchKernelGGL(sw_rerank_kernel<256>, dim3(grid), dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(sw_score_kernel<256>, dim3(grid), dim3(128), 0, stream, a);
         break;
     }
+    DRM_HIP_CHECK(hipGetLastError());
+    int tpb = 64;
+    while (tpb > 1 && (size_t)tpb * (size_t)(cmax + 1) * 4 > 65536)
+        tpb >>= 1;
+    const int64_t blocks = (a.nq + tpb - 1) / tpb;
+    hipLaunchKernelGGL(sw_topk_kernel, dim3((unsigned)blocks), dim3(tpb), (size_t)tpb * (size_t)(cmax + 1) * 4, stream,
+                       a);
     DRM_HIP_CHECK(hipGetLastError());
 }
 
@@ -337,8 +391,8 @@ void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *
         hipLaunchKernelGGL(sw_pairs_kernel<64>, dim3(grid), dim3(64), 0, stream, d_s1, d_off1, d_len1, d_s2, d_off2,
                            d_len2, npairs, d_scores);
         break;
-    case 160:
-        hipLaunchKernelGGL(sw_pairs_kernel<160>, dim3(grid), dim3(64), 0, stream, d_s1, d_off1, d_len1, d_s2,
+    case 152:
+        hipLaunchKernelGGL(sw_pairs_kernel<152>, dim3(grid), dim3(64), 0, stream, d_s1, d_off1, d_len1, d_s2,
                            d_off2, d_len2, npairs, d_scores);
         break;
     default:

@@ -44,12 +44,13 @@ class HnswPqIndex:
         check(lib().drm_search(self.handle, ptr(x), n, d, int(k), int(ef), ptr(D), ptr(I), C.byref(st)))
         return D, I, st
 
-    def search_device(self, d_x, n, k, ef, d_D, d_I, d_ndis=None, d_nhops=None, stream=None):
+    def search_device(self, d_x, n, k, ef, d_D, d_I, d_ndis=None, d_nhops=None, stream=None, d_nhops_upper=None):
         """Search on device buffers (DeviceBuffer), enqueued on `stream`."""
-        check(lib().drm_search_device(self.handle, d_x.ptr, int(n), int(k), int(ef), d_D.ptr, d_I.ptr,
-                                      d_ndis.ptr if d_ndis is not None else None,
-                                      d_nhops.ptr if d_nhops is not None else None,
-                                      stream.handle if stream is not None else None))
+        check(lib().drm_search_device_ex(self.handle, d_x.ptr, int(n), int(k), int(ef), d_D.ptr, d_I.ptr,
+                                         d_ndis.ptr if d_ndis is not None else None,
+                                         d_nhops.ptr if d_nhops is not None else None,
+                                         d_nhops_upper.ptr if d_nhops_upper is not None else None,
+                                         stream.handle if stream is not None else None))
 
     def free(self):
         if self._h:

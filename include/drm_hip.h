@@ -90,6 +90,10 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
  * ndis / nhops ([n] int32, may be NULL) receive the per-query HNSWStats the kernel measured. */
 int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                       int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, void *stream);
+/* As drm_search_device, plus d_nhops_upper[n] (may be NULL): the greedy hops on levels >= 1
+ * contained in nhops (they read M_hnsw-wide rows instead of 2*M_hnsw-wide ones). */
+int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                         int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, void *stream);
 
 /* ---------------------------------------------------------------- Smith-Waterman rerank */
 /* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):
