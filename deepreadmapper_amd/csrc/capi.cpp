@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -216,6 +217,13 @@ int drm_index_load(const char *path, int device, drm_index **out)
             }
         }
         d.upper_len = (int64_t)upper.size();
+        // tuning knobs: visited-set placement, speculative code loads, kernel choice
+        if (const char *e = std::getenv("DRM_SEARCH_VMODE"))
+            d.vmode = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_SPEC"))
+            d.spec_codes = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
+            d.force_lds_kernel = std::atoi(e) ? 1 : 0;
         try {
             d.centroids = upload_vec(h.centroids, d.device_bytes);
             d.codes = upload_vec(h.codes, d.device_bytes);

@@ -27,6 +27,9 @@ struct DeviceIndex {
     int32_t deg0 = 0, n_levels = 0, max_level = -1, entry_point = -1;
     int32_t cum[kMaxLevels + 1] = {};
     int32_t has_dup_links = 0; // some neighbour row lists one id twice
+    int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
+    int32_t spec_codes = 1;    // issue PQ code loads before the visited test
+    int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
     uint8_t *codes = nullptr;      // [ntotal][code_size]
     int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
@@ -73,6 +76,8 @@ struct SearchArgs {
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
+void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
+                            int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------- SW rerank
 struct DeviceRefs {

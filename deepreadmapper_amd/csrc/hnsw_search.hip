@@ -35,10 +35,17 @@ struct DI {
     int32_t i;
 };
 
+// Distances are compared through an order-preserving uint32 image (ord32), so every heap
+// comparison is integer and runs on the scalar unit: float a < b  <=>  ord32(a) < ord32(b)
+// (no NaN, and +0 only: distances are sums of squares starting from +0.0f).
 __device__ __forceinline__ uint32_t ord32(float f)
 {
     uint32_t u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord32(uint32_t o)
+{
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
@@ -52,100 +59,231 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
     }
     return v;
 }
-
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
+__device__ __forceinline__ uint32_t ufirst(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
-__device__ __forceinline__ int prefix_count(uint64_t mask, int lane)
+// faiss::CMax<float, TI>::cmp2 on (ord32 key, id)
+__device__ __forceinline__ bool cmp2(uint32_t k1, uint32_t k2, int32_t i1, int32_t i2)
 {
-    return __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    return (k1 > k2) || ((k1 == k2) && (i1 > i2));
 }
 
-// faiss::CMax<float, TI>::cmp2
-__device__ __forceinline__ bool cmp2(float v1, float v2, int32_t i1, int32_t i2)
+// Register-resident arrays of 64*R slots: slot s lives in lane (s & 63), register (s >> 6).
+// rd/wr take a wave-uniform slot: rd compiles to v_readlane, wr to a lane-masked v_cndmask.
+template <int R> __device__ __forceinline__ uint32_t rd(const uint32_t (&a)[R], int s)
 {
-    return (v1 > v2) || ((v1 == v2) && (i1 > i2));
+    const int l = s & 63, r = s >> 6;
+    uint32_t out = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)a[i], l);
+        out = (r == i) ? x : out;
+    }
+    return out;
+}
+template <int R> __device__ __forceinline__ void wr(uint32_t (&a)[R], int s, uint32_t v)
+{
+    const int l = s & 63, r = s >> 6;
+    const bool mine = (int)(threadIdx.x & 63) == l; // v_cmp + v_cndmask (no writelane builtin in HIP)
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+        if (r == i)
+            a[i] = mine ? v : a[i];
 }
 
-// faiss heap_push<CMax<float,int32>>(k, ...) on a 0-based LDS array (1-based internally)
-__device__ void heap_push(DI *h, int k, float val, int32_t id)
+// faiss heap_push<CMax<float,int32>>(k, ...) -- the MinimaxHeap layout, replayed exactly
+template <int R> __device__ void heap_push(uint32_t (&hk)[R], uint32_t (&hi)[R], int k, uint32_t key, int32_t id)
 {
     int i = k;
     while (i > 1) {
-        int f = i >> 1;
-        DI pf = h[f - 1];
-        if (!cmp2(val, pf.d, id, pf.i))
+        const int f = i >> 1;
+        const uint32_t pk = rd(hk, f - 1);
+        const int32_t pi = (int32_t)rd(hi, f - 1);
+        if (!cmp2(key, pk, id, pi))
             break;
-        h[i - 1] = pf;
+        wr(hk, i - 1, pk);
+        wr(hi, i - 1, (uint32_t)pi);
         i = f;
     }
-    h[i - 1] = DI{val, id};
+    wr(hk, i - 1, key);
+    wr(hi, i - 1, (uint32_t)id);
 }
 
 // faiss heap_pop<CMax<float,int32>>(k, ...)
-__device__ void heap_pop(DI *h, int k)
+template <int R> __device__ void heap_pop(uint32_t (&hk)[R], uint32_t (&hi)[R], int k)
 {
-    DI last = h[k - 1];
+    const uint32_t lk = rd(hk, k - 1);
+    const int32_t li = (int32_t)rd(hi, k - 1);
     int i = 1;
     for (;;) {
-        int i1 = i << 1, i2 = i1 + 1;
+        const int i1 = i << 1, i2 = i1 + 1;
         if (i1 > k)
             break;
-        DI c1 = h[i1 - 1];
-        DI c2 = (i2 <= k) ? h[i2 - 1] : c1;
-        if ((i2 == k + 1) || cmp2(c1.d, c2.d, c1.i, c2.i)) {
-            if (cmp2(last.d, c1.d, last.i, c1.i))
+        const uint32_t k1 = rd(hk, i1 - 1);
+        const int32_t d1 = (int32_t)rd(hi, i1 - 1);
+        uint32_t k2 = k1;
+        int32_t d2 = d1;
+        if (i2 <= k) {
+            k2 = rd(hk, i2 - 1);
+            d2 = (int32_t)rd(hi, i2 - 1);
+        }
+        if ((i2 == k + 1) || cmp2(k1, k2, d1, d2)) {
+            if (cmp2(lk, k1, li, d1))
                 break;
-            h[i - 1] = c1;
+            wr(hk, i - 1, k1);
+            wr(hi, i - 1, (uint32_t)d1);
             i = i1;
         } else {
-            if (cmp2(last.d, c2.d, last.i, c2.i))
+            if (cmp2(lk, k2, li, d2))
                 break;
-            h[i - 1] = c2;
+            wr(hk, i - 1, k2);
+            wr(hi, i - 1, (uint32_t)d2);
             i = i2;
         }
     }
-    h[i - 1] = h[k - 1];
+    wr(hk, i - 1, lk);
+    wr(hi, i - 1, (uint32_t)li);
 }
 
-// faiss heap_replace_top<CMax<float,int64>>(k, ...) -- labels are storage ids (< 2^31)
-__device__ void heap_replace_top(DI *h, int k, float val, int32_t id)
+// ---- DPP wave reductions (gfx9 DPP: row_shr:1/2/4/8, row_bcast:15/31, wave_shr:1)
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v, int ctrl, int row_mask)
 {
-    int i = 1;
-    for (;;) {
-        int i1 = i << 1, i2 = i1 + 1;
-        if (i1 > k)
-            break;
-        DI c1 = h[i1 - 1];
-        DI c2 = (i2 <= k) ? h[i2 - 1] : c1;
-        if ((i2 == k + 1) || cmp2(c1.d, c2.d, c1.i, c2.i)) {
-            if (cmp2(val, c1.d, id, c1.i))
-                break;
-            h[i - 1] = c1;
-            i = i1;
-        } else {
-            if (cmp2(val, c2.d, id, c2.i))
-                break;
-            h[i - 1] = c2;
-            i = i2;
+    switch (ctrl) { // the builtin needs compile-time controls
+    case 0x111: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x111, 0xF, 0xF, false);
+    case 0x112: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x112, 0xF, 0xF, false);
+    case 0x114: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x114, 0xF, 0xF, false);
+    case 0x118: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x118, 0xF, 0xF, false);
+    case 0x142: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x142, 0xA, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x143, 0xC, 0xF, false);
+    }
+}
+// min over the 64 lanes, returned wave-uniform
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x111, 0xF));
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x112, 0xF));
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x114, 0xF));
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x118, 0xF));
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x142, 0xA));
+    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x143, 0xC));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// lexicographic min of (hi, lo) over the wave
+__device__ __forceinline__ uint64_t wave_min_pair(uint32_t hi, uint32_t lo)
+{
+    const uint32_t mh = wave_min_u32(hi);
+    const uint32_t ml = wave_min_u32(hi == mh ? lo : 0xFFFFFFFFu);
+    return ((uint64_t)mh << 32) | ml;
+}
+// lane i <- lane i-1 (lane 0 <- old)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t old, uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+// value of register array `a` at a per-lane slot (ds_bpermute per register)
+template <int R> __device__ __forceinline__ uint32_t fetch(const uint32_t (&a)[R], int slot)
+{
+    const int sl = slot & 63, sr = slot >> 6;
+    uint32_t out = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t x = (uint32_t)__shfl((int)a[r], sl, 64);
+        out = (sr == r) ? x : out;
+    }
+    return out;
+}
+
+// faiss heap_push<CMax<float,int32>>(k, val, id), wave-parallel (R <= 2, k <= 64R <= 128):
+// lane l >= 1 holds the ancestor at level l; the sift-up stops at the first ancestor that does
+// not compare below val; every lane then pulls the new contents of its path slots.
+template <int R> __device__ void heap_push_par(uint32_t (&hk)[R], uint32_t (&hi)[R], int k, uint32_t key, int32_t id)
+{
+    const int lane = lane_id();
+    const int anc = (lane < 16) ? (k >> lane) : 0;
+    const bool exists = lane >= 1 && anc >= 1;
+    const int src = exists ? anc - 1 : 0;
+    const uint32_t ak = fetch(hk, src);
+    const int32_t ai = (int32_t)fetch(hi, src);
+    const bool moves = exists && cmp2(key, ak, id, ai);
+    const uint64_t stopm = __ballot(lane >= 1 && !moves);
+    const int h = __builtin_ctzll(stopm) - 1; // parents moved down; val lands at k >> h
+    const int bk = 32 - __builtin_clz((unsigned)k);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int p = lane + 64 * r + 1;
+        const int m = bk - (32 - __builtin_clz((unsigned)p));
+        const bool on = m >= 0 && m <= h && (k >> m) == p;
+        const int srcl = (m + 1) & 63;
+        const uint32_t vk = (uint32_t)__shfl((int)ak, srcl, 64);
+        const int32_t vi = __shfl(ai, srcl, 64);
+        if (on) {
+            hk[r] = (m == h) ? key : vk;
+            hi[r] = (m == h) ? (uint32_t)id : (uint32_t)vi;
         }
     }
-    h[i - 1] = DI{val, id};
+}
+
+// faiss heap_pop<CMax<float,int32>>(k), wave-parallel (R <= 2): lane p-1 decides which child the
+// sift-down takes at internal node p, lane l walks to the path node at depth l, the hole stops at
+// the first child that `last` does not compare below, and owners pull their new slot contents.
+template <int R> __device__ void heap_pop_par(uint32_t (&hk)[R], uint32_t (&hi)[R], int k)
+{
+    const int lane = lane_id();
+    const uint32_t lk = rd(hk, k - 1);
+    const int32_t li = (int32_t)rd(hi, k - 1);
+    const int c1 = 2 * (lane + 1), c2 = c1 + 1;
+    const int s1 = min(c1, 64 * R) - 1, s2 = min(c2, 64 * R) - 1;
+    const uint32_t k1 = fetch(hk, s1), k2 = fetch(hk, s2);
+    const int32_t i1 = (int32_t)fetch(hi, s1), i2 = (int32_t)fetch(hi, s2);
+    const uint64_t lm = __ballot((c2 == k + 1) || cmp2(k1, k2, i1, i2)); // bit p-1: take left child
+    int pl = 1;
+    bool exists = true;
+    for (int t = 0; t < 12; ++t) {
+        if (t >= lane)
+            break;
+        if (2 * pl > k) {
+            exists = false;
+            break;
+        }
+        pl = 2 * pl + (int)(((lm >> (pl - 1)) & 1ull) ^ 1ull);
+    }
+    const bool onpath = lane < 12 && exists;
+    const int src = onpath ? pl - 1 : 0;
+    const uint32_t ak = fetch(hk, src);
+    const int32_t ai = (int32_t)fetch(hi, src);
+    const uint64_t sm = __ballot(lane >= 1 && (!onpath || cmp2(lk, ak, li, ai)));
+    const int h = __builtin_ctzll(sm) - 1; // the hole ends at path depth h
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int pos = lane + 64 * r + 1;
+        const int m = 31 - __builtin_clz((unsigned)pos);
+        const int pm = __shfl(pl, m & 63, 64);
+        const bool on = m <= h && pm == pos;
+        const int srcl = (m + 1) & 63;
+        const uint32_t vk = (uint32_t)__shfl((int)ak, srcl, 64);
+        const int32_t vi = __shfl(ai, srcl, 64);
+        if (on) {
+            hk[r] = (m == h) ? lk : vk;
+            hi[r] = (m == h) ? (uint32_t)li : (uint32_t)vi;
+        }
+    }
 }
 
 // PQ ADC distance of node v: sequential fp32 sum over sub-quantizers starting from 0
 // (distance_single_code / distance_four_codes for M < 16) [upstream faiss].
 template <bool FAST8>
-__device__ __forceinline__ float pq_distance(const SearchArgs &a, const float *lut, int32_t v)
+__device__ __forceinline__ float pq_distance_code(const SearchArgs &a, const float *lut, int32_t v, uint2 c8)
 {
     float r = 0.0f;
-    if (FAST8) { // M == 8, nbits == 8: one 8-byte code load
-        const uint2 c = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v * 8);
+    if (FAST8) { // M == 8, nbits == 8: the 8-byte code is already in c8
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            r = __fadd_rn(r, lut[m * 256 + ((c.x >> (8 * m)) & 255u)]);
+            r = __fadd_rn(r, lut[m * 256 + ((c8.x >> (8 * m)) & 255u)]);
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            r = __fadd_rn(r, lut[(m + 4) * 256 + ((c.y >> (8 * m)) & 255u)]);
+            r = __fadd_rn(r, lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)]);
         return r;
     }
     const uint8_t *code = a.codes + (size_t)v * a.code_size;
@@ -154,9 +292,9 @@ __device__ __forceinline__ float pq_distance(const SearchArgs &a, const float *l
         if (a.nbits == 8) {
             idx = code[m];
         } else {
-            uint32_t bitpos = (uint32_t)m * (uint32_t)a.nbits;
-            uint32_t byte = bitpos >> 3, shift = bitpos & 7;
-            uint32_t need = shift + (uint32_t)a.nbits;
+            const uint32_t bitpos = (uint32_t)m * (uint32_t)a.nbits;
+            const uint32_t byte = bitpos >> 3, shift = bitpos & 7;
+            const uint32_t need = shift + (uint32_t)a.nbits;
             uint32_t acc = 0;
             for (uint32_t b = 0; b * 8 < need; ++b)
                 acc |= (uint32_t)code[byte + b] << (8 * b);
@@ -167,37 +305,44 @@ __device__ __forceinline__ float pq_distance(const SearchArgs &a, const float *l
     return r;
 }
 
-template <bool FAST8>
+template <bool FAST8> __device__ __forceinline__ uint2 load_code8(const SearchArgs &a, int32_t v)
+{
+    if (FAST8)
+        return *reinterpret_cast<const uint2 *>(a.codes + (size_t)v * 8);
+    return make_uint2(0u, 0u);
+}
+
+constexpr int kHashSlots = 2048; // LDS visited hash per wave (8 KB)
+
+__device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - 11); }
+
+// VMODE 0: visited = per-slot HBM bitmap (atomicOr test-and-set).
+// VMODE 1: visited = LDS open-addressing hash; when it nears capacity the query spills it into the
+//          HBM bitmap and continues there (exact in both regimes).
+template <int R, bool FAST8, int VMODE, bool SPEC>
 __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
-    // LDS carve-up (all offsets 16-byte aligned by construction on the host)
     float *lut = reinterpret_cast<float *>(smem);
     float *qv = lut + a.M * a.ksub;
-    DI *cand = reinterpret_cast<DI *>(qv + ((a.d + 3) & ~3));
-    DI *res = cand + ((a.ef + 1) & ~1);
-    DI *nb = res + a.kpad;                                // 64 entries
-    uint64_t *keys = reinterpret_cast<uint64_t *>(res);  // sort image, aliases res
+    int32_t *ht = reinterpret_cast<int32_t *>(qv + ((a.d + 3) & ~3)); // visited hash (VMODE 1)
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
+    const uint32_t kInfKey = ord32(INFINITY);
 
     for (;;) {
-        int64_t q = 0;
+        int q = 0;
         if (lane == 0)
-            q = (int64_t)atomicAdd(a.counter, 1u);
-        q = (int64_t)__builtin_amdgcn_readfirstlane((int)q);
-        if (q >= a.n)
+            q = (int)atomicAdd(a.counter, 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if ((int64_t)q >= a.n)
             break;
 
-        int32_t ndis = 0, nhops = 0;
-        // --- HeapBlockResultHandler::begin: heapify k x (+inf, -1)
-        for (int j = lane; j < a.k; j += 64)
-            res[j] = DI{INFINITY, -1};
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < a.k; j += 64) {
-                a.D[q * a.k + j] = INFINITY;
-                a.I[q * a.k + j] = -1;
+                a.D[(int64_t)q * a.k + j] = INFINITY;
+                a.I[(int64_t)q * a.k + j] = -1;
             }
             if (lane == 0) {
                 a.ndis[q] = 0;
@@ -207,9 +352,14 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             }
             continue;
         }
-        // --- set_query: query vector to LDS, then LUT[m][c] = sum_t (x - c)^2 (sequential t)
+        // --- set_query: LUT[m][c] = sum_t (x - c)^2, sequential t, no FMA
         for (int t = lane; t < a.d; t += 64)
-            qv[t] = a.x[q * a.d + t];
+            qv[t] = a.x[(int64_t)q * a.d + t];
+        if (VMODE == 1) {
+            int4 *h4 = reinterpret_cast<int4 *>(ht);
+            for (int t = lane; t < kHashSlots / 4; t += 64)
+                h4[t] = make_int4(-1, -1, -1, -1);
+        }
         __syncthreads();
         for (int e = lane; e < a.M * a.ksub; e += 64) {
             const int m = e / a.ksub;
@@ -217,107 +367,180 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             const float *xs = qv + m * a.dsub;
             float acc = 0.0f;
             for (int t = 0; t < a.dsub; ++t) {
-                float diff = __fsub_rn(xs[t], cen[t]);
+                const float diff = __fsub_rn(xs[t], cen[t]);
                 acc = __fadd_rn(acc, __fmul_rn(diff, diff));
             }
             lut[e] = acc;
         }
         __syncthreads();
 
-        // --- greedy descent on levels max_level .. 1 (greedy_update_nearest)
+        // --- greedy_update_nearest on levels max_level .. 1
         int32_t nearest = a.entry_point;
-        float d_nearest = pq_distance<FAST8>(a, lut, nearest);
+        uint32_t dn = ufirst(ord32(pq_distance_code<FAST8>(a, lut, nearest, load_code8<FAST8>(a, nearest))));
+        int ndis = 0, nhops = 0;
         for (int level = a.max_level; level >= 1; --level) {
             const int cnt = a.cum[level + 1] - a.cum[level];
             for (;;) {
                 const int32_t prev = nearest;
                 const uint32_t base = a.upper_off[nearest] + (uint32_t)(a.cum[level] - a.cum[1]);
-                int32_t v = (lane < cnt) ? a.upper_nbr[base + lane] : -1;
+                const int32_t v = (lane < cnt) ? a.upper_nbr[base + lane] : -1;
                 const uint64_t neg = __ballot(lane < cnt && v < 0);
                 const int nvalid = neg ? (__ffsll((unsigned long long)neg) - 1) : cnt;
-                float dd = INFINITY;
+                uint32_t dk = 0xFFFFFFFFu;
                 if (lane < nvalid)
-                    dd = pq_distance<FAST8>(a, lut, v);
+                    dk = ord32(pq_distance_code<FAST8>(a, lut, v, load_code8<FAST8>(a, v)));
                 ndis += nvalid;
                 nhops += 1;
                 // sequential `if (dis < d_nearest)` in link order == first lane holding the minimum
-                uint64_t key = (lane < nvalid) ? (((uint64_t)ord32(dd) << 32) | (uint32_t)lane) : ~0ull;
+                uint64_t key = (lane < nvalid) ? (((uint64_t)dk << 32) | (uint32_t)lane) : ~0ull;
                 key = wave_min_u64(key);
                 if (key != ~0ull) {
-                    const int bl = (int)(key & 63);
-                    const float bd = __shfl(dd, bl, 64);
-                    const int32_t bv = __shfl(v, bl, 64);
-                    if (bd < d_nearest) {
-                        d_nearest = bd;
-                        nearest = bv;
+                    const uint32_t bk = (uint32_t)(key >> 32);
+                    if (bk < dn) {
+                        dn = bk;
+                        nearest = __builtin_amdgcn_readlane(v, (int)(key & 63));
                     }
                 }
                 if (nearest == prev)
                     break;
             }
         }
+        const int nhops_upper = nhops;
 
-        // --- level 0: MinimaxHeap candidates(ef); push(nearest); seed result + visited
-        int kc = 1, nvalid = 1;
-        if (lane == 0)
-            cand[0] = DI{d_nearest, nearest};
-        float thr = INFINITY;
-        if (lane == 0) {
-            if (d_nearest < thr) {
-                heap_replace_top(res, a.k, d_nearest, nearest);
-                thr = res[0].d;
+        // --- level 0. Result handler: k slots of (+inf,-1) (HeapBlockResultHandler::begin)
+        uint32_t rk[R], ri[R], ck[R], ci[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            rk[r] = kInfKey;
+            ri[r] = 0xFFFFFFFFu;
+            ck[r] = 0;
+            ci[r] = 0xFFFFFFFFu;
+        }
+        // Result set kept sorted by (key, id) in slots 0..k-1: inserting below the max (slot k-1)
+        // evicts the max, which is exactly heap_replace_top's effect on the k-set; the output order
+        // is heap_reorder's (valid entries ascending, then (+inf,-1)).
+        uint32_t thr = kInfKey;
+        auto add_result = [&](uint32_t key, int32_t id) {
+            if (key < thr) { // SingleResultHandler::add_result: strict on distance
+                int pos = 0;
+                uint32_t pk[R], pi[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    pos += __popcll(__ballot((lane + 64 * r) < a.k && cmp2(key, rk[r], id, (int32_t)ri[r])));
+                    const uint32_t carry_k = r ? (uint32_t)__builtin_amdgcn_readlane((int)rk[r - 1], 63) : 0u;
+                    const uint32_t carry_i = r ? (uint32_t)__builtin_amdgcn_readlane((int)ri[r - 1], 63) : 0u;
+                    pk[r] = wave_shr1(carry_k, rk[r]);
+                    pi[r] = wave_shr1(carry_i, ri[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int s = lane + 64 * r;
+                    if (s > pos) {
+                        rk[r] = pk[r];
+                        ri[r] = pi[r];
+                    } else if (s == pos) {
+                        rk[r] = key;
+                        ri[r] = (uint32_t)id;
+                    }
+                }
+                thr = rd(rk, a.k - 1);
             }
+        };
+        // MinimaxHeap candidates(ef); push(nearest, d_nearest); seed result + visited set
+        int kc = 1, nvalid = 1;
+        wr(ck, 0, dn);
+        wr(ci, 0, (uint32_t)nearest);
+        add_result(dn, nearest);
+        int clear_n = 0, hcount = 0;
+        bool spilled = (VMODE == 0);
+        if (VMODE == 1) {
+            if (lane == 0)
+                ht[vhash(nearest)] = nearest;
+            hcount = 1;
+        } else {
+            if (lane == 0) {
+                atomicOr(&vis[nearest >> 5], 1u << (nearest & 31));
+                if (a.clear_cap > 0)
+                    clr[0] = nearest;
+            }
+            clear_n = 1;
         }
-        thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(thr)));
-        int clear_n = 0;
-        if (lane == 0) {
-            atomicOr(&vis[nearest >> 5], 1u << (nearest & 31));
-            if (a.clear_cap > 0)
-                clr[0] = nearest;
-        }
-        clear_n = 1;
         __syncthreads();
 
         int nstep = 0, ndis0 = 0;
         while (nvalid > 0) {
-            // pop_min: min distance over valid slots, ties -> highest slot
-            uint64_t best = ~0ull;
-            for (int s = lane; s < kc; s += 64) {
-                const DI e = cand[s];
-                if (e.i != -1) {
-                    uint64_t key = ((uint64_t)ord32(e.d) << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)s);
-                    best = key < best ? key : best;
+            // pop_min: smallest distance among valid slots, ties -> highest slot
+            uint32_t bh = 0xFFFFFFFFu, bl = 0xFFFFFFFFu;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int s = lane + 64 * r;
+                if (s < kc && ci[r] != 0xFFFFFFFFu) {
+                    const uint32_t lo = 0xFFFFFFFFu - (uint32_t)s;
+                    if (ck[r] < bh || (ck[r] == bh && lo < bl)) {
+                        bh = ck[r];
+                        bl = lo;
+                    }
                 }
             }
-            best = wave_min_u64(best);
-            const int imin = (int)(0xFFFFFFFFu - (uint32_t)best);
-            const DI pm = cand[imin];
-            const float d0 = pm.d;
-            const int32_t v0 = pm.i;
-            __syncthreads();
-            if (lane == 0)
-                cand[imin].i = -1;
+            const uint64_t best = wave_min_pair(bh, bl);
+            const int imin = (int)ufirst(0xFFFFFFFFu - (uint32_t)best);
+            const uint32_t d0 = ufirst((uint32_t)(best >> 32));
+            const int32_t v0 = (int32_t)rd(ci, imin);
+            wr(ci, imin, 0xFFFFFFFFu);
             nvalid--;
             // count_below(d0): every slot < kc, popped ones included
             int below = 0;
-            for (int base = 0; base < kc; base += 64) {
-                const int s = base + lane;
-                const bool b = (s < kc) && (cand[s].d < d0);
-                below += __popcll(__ballot(b));
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int s = lane + 64 * r;
+                below += __popcll(__ballot(s < kc && ck[r] < d0));
             }
             if (below >= a.efSearch)
                 break;
 
-            // expand v0's level-0 row
-            const int32_t *row = a.nbr0 + (size_t)v0 * (size_t)a.deg0;
-            const int32_t v1 = (lane < a.deg0) ? row[lane] : -1;
+            // expand v0's level-0 row (one coalesced 128-B load at M_hnsw = 16)
+            const int32_t v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
             const uint64_t negm = __ballot(lane < a.deg0 && v1 < 0);
             const int jmax = negm ? (__ffsll((unsigned long long)negm) - 1) : a.deg0;
+            const bool act = lane < jmax;
+            uint2 c8 = make_uint2(0u, 0u);
+            if (SPEC && FAST8 && act)
+                c8 = load_code8<FAST8>(a, v1); // issued before the visited test: overlaps its latency
+            if (VMODE == 1 && !spilled && hcount + jmax > (kHashSlots * 7) / 8) {
+                // spill the LDS set into the HBM bitmap + clear list, continue there
+                for (int t = lane; t < kHashSlots; t += 64) {
+                    const int32_t hv = ht[t];
+                    const bool has = hv >= 0;
+                    const uint64_t m = __ballot(has);
+                    if (has) {
+                        atomicOr(&vis[hv >> 5], 1u << (hv & 31));
+                        const int p = clear_n + __popcll(m & lanes_below(lane));
+                        if (p < a.clear_cap)
+                            clr[p] = hv;
+                    }
+                    clear_n += __popcll(m);
+                }
+                spilled = true;
+            }
             bool fresh = false;
-            if (lane < jmax) {
-                const uint32_t bit = 1u << (v1 & 31);
-                const uint32_t old = atomicOr(&vis[v1 >> 5], bit);
-                fresh = (old & bit) == 0u;
+            if (act) {
+                if (VMODE == 1 && !spilled) {
+                    uint32_t h = vhash(v1);
+                    for (;;) {
+                        const int32_t old = atomicCAS(&ht[h], -1, v1);
+                        if (old == -1) {
+                            fresh = true;
+                            break;
+                        }
+                        if (old == v1)
+                            break;
+                        h = (h + 1) & (kHashSlots - 1);
+                    }
+                } else {
+                    const uint32_t bit = 1u << (v1 & 31);
+                    const uint32_t old = atomicOr(&vis[v1 >> 5], bit);
+                    fresh = (old & bit) == 0u;
+                }
             }
             if (a.check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
@@ -328,94 +551,80 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             }
             const uint64_t fm = __ballot(fresh);
             const int nf = __popcll(fm);
-            const int pos = prefix_count(fm, lane);
+            if (spilled && fresh) {
+                const int p = clear_n + __popcll(fm & lanes_below(lane));
+                if (p < a.clear_cap)
+                    clr[p] = v1;
+            }
+            if (spilled)
+                clear_n += nf;
+            else
+                hcount += nf;
+            uint32_t dk = 0;
             if (fresh) {
-                if (clear_n + pos < a.clear_cap)
-                    clr[clear_n + pos] = v1;
-                const float dd = pq_distance<FAST8>(a, lut, v1);
-                nb[pos] = DI{dd, v1};
+                if (!(SPEC && FAST8))
+                    c8 = load_code8<FAST8>(a, v1);
+                dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
             }
-            clear_n += nf;
             ndis0 += nf;
-            __syncthreads();
-            if (lane == 0) {
-                // add_to_heap for each fresh link, in row order
-                for (int t = 0; t < nf; ++t) {
-                    const DI e = nb[t];
-                    if (e.d < thr) {
-                        heap_replace_top(res, a.k, e.d, e.i);
-                        thr = res[0].d;
-                    }
-                    // MinimaxHeap::push
-                    if (kc == a.ef) {
-                        const DI top = cand[0];
-                        if (e.d >= top.d)
-                            continue;
-                        if (top.i != -1)
-                            --nvalid;
-                        heap_pop(cand, kc--);
-                    }
-                    heap_push(cand, ++kc, e.d, e.i);
-                    ++nvalid;
+            // add_to_heap for each fresh link in row order (wave-uniform scalar loop)
+            uint64_t rem = fm;
+            while (rem) {
+                const int l = __builtin_ctzll(rem);
+                rem &= rem - 1;
+                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
+                const int32_t id = __builtin_amdgcn_readlane(v1, l);
+                add_result(key, id);
+                if (kc == a.ef) { // MinimaxHeap::push on a full heap
+                    if (key >= (uint32_t)__builtin_amdgcn_readlane((int)ck[0], 0))
+                        continue;
+                    if ((uint32_t)__builtin_amdgcn_readlane((int)ci[0], 0) != 0xFFFFFFFFu)
+                        --nvalid;
+                    if (R <= 2)
+                        heap_pop_par(ck, ci, kc);
+                    else
+                        heap_pop(ck, ci, kc);
+                    kc--;
                 }
+                kc++;
+                if (R <= 2)
+                    heap_push_par(ck, ci, kc, key, id);
+                else
+                    heap_push(ck, ci, kc, key, id);
+                ++nvalid;
             }
-            kc = __builtin_amdgcn_readfirstlane(kc);
-            nvalid = __builtin_amdgcn_readfirstlane(nvalid);
-            thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(thr)));
-            __syncthreads();
             nstep++;
         }
 
-        // --- SingleResultHandler::end (heap_reorder): ascending (distance, id), (+inf,-1) padding
-        __syncthreads();
-        for (int j = lane; j < a.kpad; j += 64) { // in place: keys[j] aliases res[j] (both 8 bytes)
-            const DI e = (j < a.k) ? res[j] : DI{INFINITY, -1};
-            keys[j] = (e.i >= 0) ? (((uint64_t)ord32(e.d) << 32) | (uint32_t)e.i) : ~0ull;
-        }
-        __syncthreads();
-        for (int size = 2; size <= a.kpad; size <<= 1) {
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                for (int t = lane; t < (a.kpad >> 1); t += 64) {
-                    const int i = 2 * t - (t & (stride - 1));
-                    const int j = i + stride;
-                    const bool asc = (i & size) == 0;
-                    const uint64_t x = keys[i], y = keys[j];
-                    if ((x > y) == asc) {
-                        keys[i] = y;
-                        keys[j] = x;
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int j = lane; j < a.k; j += 64) {
-            const uint64_t key = keys[j];
-            if (key == ~0ull) {
-                a.D[q * a.k + j] = INFINITY;
-                a.I[q * a.k + j] = -1;
-            } else {
-                const uint32_t o = (uint32_t)(key >> 32);
-                const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
-                a.D[q * a.k + j] = __uint_as_float(u);
-                a.I[q * a.k + j] = (int64_t)(uint32_t)key;
+        // --- SingleResultHandler::end (heap_reorder): the sorted slots are already its output
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int j = lane + 64 * r;
+            if (j < a.k) {
+                const int64_t o = (int64_t)q * a.k + j;
+                const bool valid = (int32_t)ri[r] >= 0;
+                a.D[o] = valid ? unord32(rk[r]) : INFINITY;
+                a.I[o] = valid ? (int64_t)(int32_t)ri[r] : (int64_t)-1;
             }
         }
         if (lane == 0) {
             a.ndis[q] = ndis + ndis0;
             a.nhops[q] = nhops + nstep;
             if (a.nhops_upper)
-                a.nhops_upper[q] = nhops;
+                a.nhops_upper[q] = nhops_upper;
         }
 
-        // --- VisitedTable::advance: clear exactly the bits this query set
-        if (clear_n <= a.clear_cap) {
-            for (int t = lane; t < clear_n; t += 64)
-                vis[clr[t] >> 5] = 0u;
-        } else {
-            for (int64_t w = lane; w < a.vis_words; w += 64)
-                vis[w] = 0u;
+        // --- VisitedTable::advance: clear exactly the HBM bits this query set
+        if (spilled) {
+            if (clear_n <= a.clear_cap) {
+                for (int t = lane; t < clear_n; t += 64)
+                    vis[clr[t] >> 5] = 0u;
+            } else {
+                for (int64_t w = lane; w < a.vis_words; w += 64)
+                    vis[w] = 0u;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 }
@@ -432,8 +641,6 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     if (ef < 1)
         ef = 1;
     const int efc = std::max(ef, k);
-    if (efc > 4096)
-        throw Error(DRM_ERR_UNSUPPORTED, "max(efSearch, k) must be <= 4096 on the GPU path");
     if (ix.deg0 > 64)
         throw Error(DRM_ERR_UNSUPPORTED, "level-0 degree 2*M_hnsw must be <= 64 on the GPU path");
     for (int l = 1; l < ix.n_levels; ++l)
@@ -445,8 +652,14 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     int kpad = 64;
     while (kpad < k)
         kpad <<= 1;
-    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub + sizeof(float) * (size_t)((ix.d + 3) & ~3) +
-                       sizeof(DI) * (size_t)((efc + 1) & ~1) + sizeof(DI) * (size_t)kpad + sizeof(DI) * 64;
+    const int R = (std::max(efc, k) + 63) / 64;
+    if (R > 8 || ix.force_lds_kernel) { // large ef / k: LDS-heap kernel
+        launch_hnsw_search_lds(ix, d_x, n, k, ef, d_D, d_I, d_ndis, d_nhops, d_nhops_upper, stream);
+        return;
+    }
+    const int vmode = ix.vmode;
+    const size_t scratch = vmode == 1 ? sizeof(int32_t) * 2048 : 0;
+    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub + sizeof(float) * (size_t)((ix.d + 3) & ~3) + scratch;
     if (lds > 160 * 1024)
         throw Error(DRM_ERR_UNSUPPORTED, "search workspace does not fit in LDS");
 
@@ -512,10 +725,27 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
 
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, sizeof(uint32_t), stream));
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
-    if (fast8)
-        hipLaunchKernelGGL(hnsw_pq_search_kernel<true>, dim3(slots), dim3(64), lds, stream, a);
-    else
-        hipLaunchKernelGGL(hnsw_pq_search_kernel<false>, dim3(slots), dim3(64), lds, stream, a);
+    const bool spec = ix.spec_codes != 0;
+#define DRM_LAUNCH(RR, F8, VM, SP)                                                                              \
+    hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, SP>), dim3(slots), dim3(64), lds, stream, a)
+#define DRM_LAUNCH_R(F8, VM, SP)                                                                                \
+    switch (R) {                                                                                                \
+    case 1: DRM_LAUNCH(1, F8, VM, SP); break;                                                                   \
+    case 2: DRM_LAUNCH(2, F8, VM, SP); break;                                                                   \
+    case 3: case 4: DRM_LAUNCH(4, F8, VM, SP); break;                                                           \
+    default: DRM_LAUNCH(8, F8, VM, SP); break;                                                                  \
+    }
+    if (fast8) {
+        if (vmode == 1) {
+            if (spec) { DRM_LAUNCH_R(true, 1, true) } else { DRM_LAUNCH_R(true, 1, false) }
+        } else {
+            if (spec) { DRM_LAUNCH_R(true, 0, true) } else { DRM_LAUNCH_R(true, 0, false) }
+        }
+    } else {
+        if (vmode == 1) { DRM_LAUNCH_R(false, 1, false) } else { DRM_LAUNCH_R(false, 0, false) }
+    }
+#undef DRM_LAUNCH_R
+#undef DRM_LAUNCH
     DRM_HIP_CHECK(hipGetLastError());
 }
 
