@@ -74,7 +74,7 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 
 void free_index(drm::DeviceIndex &d)
 {
-    void *ptrs[] = {d.centroids, d.codes, d.nbr0, d.upper_off, d.upper_nbr, d.visited, d.clear_list, d.counter};
+    void *ptrs[] = {d.centroids, d.codes, d.nbr0, d.upper_off, d.upper_nbr, d.visited, d.clear_list, d.counter, d.stamps};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -224,6 +224,11 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.spec_codes = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
             d.force_lds_kernel = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
+            if (std::atoi(e)) {
+                DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
+                DRM_HIP_CHECK(hipMemset(d.stamps, 0, 8 * sizeof(uint64_t)));
+            }
         try {
             d.centroids = upload_vec(h.centroids, d.device_bytes);
             d.codes = upload_vec(h.codes, d.device_bytes);
@@ -255,6 +260,17 @@ int drm_index_free(drm_index *index)
         (void)hipSetDevice(index->dev.device);
         free_index(index->dev);
         delete index;
+    });
+}
+
+// diagnostic (not part of include/drm_hip.h): read and reset the section timers of a stamps build
+int drm_debug_search_stamps(drm_index *index, uint64_t *out8)
+{
+    return guarded([&] {
+        if (!index || !index->dev.stamps)
+            throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
+        DRM_HIP_CHECK(hipMemcpy(out8, index->dev.stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 8 * sizeof(uint64_t)));
     });
 }
 

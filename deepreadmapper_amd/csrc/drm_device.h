@@ -30,6 +30,7 @@ struct DeviceIndex {
     int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
     int32_t spec_codes = 1;    // issue PQ code loads before the visited test
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
+    uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
     uint8_t *codes = nullptr;      // [ntotal][code_size]
     int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
@@ -72,6 +73,7 @@ struct SearchArgs {
     int32_t clear_cap;
     uint32_t *counter;
     int32_t check_dups;
+    uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1), else null
 };
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,

@@ -312,6 +312,13 @@ template <bool FAST8> __device__ __forceinline__ uint2 load_code8(const SearchAr
     return make_uint2(0u, 0u);
 }
 
+// Each bitmap slot is owned by exactly one workgroup (one wave) for the whole launch, so a
+// workgroup-scope atomic is sufficient: it is performed in the XCD's L2 instead of memory-side.
+__device__ __forceinline__ uint32_t vis_test_set(uint32_t *w, uint32_t bit)
+{
+    return __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 constexpr int kHashSlots = 2048; // LDS visited hash per wave (8 KB)
 
 __device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - 11); }
@@ -319,10 +326,24 @@ __device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9
 // VMODE 0: visited = per-slot HBM bitmap (atomicOr test-and-set).
 // VMODE 1: visited = LDS open-addressing hash; when it nears capacity the query spills it into the
 //          HBM bitmap and continues there (exact in both regimes).
-template <int R, bool FAST8, int VMODE, bool SPEC>
+// STAMPS (diagnostic builds only): per-section s_memtime sums -> a.stamps[section], for time shares.
+#define DRM_STAMP(idx)                                                                                      \
+    do {                                                                                                    \
+        if (STAMPS) {                                                                                       \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                                               \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            st_acc[idx] += _t - st_last;                                                                    \
+            st_last = _t;                                                                                   \
+        }                                                                                                   \
+    } while (0)
+
+template <int R, bool FAST8, int VMODE, bool SPEC, bool STAMPS = false>
 __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
     float *qv = lut + a.M * a.ksub;
@@ -352,6 +373,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             }
             continue;
         }
+        DRM_STAMP(7);
         // --- set_query: LUT[m][c] = sum_t (x - c)^2, sequential t, no FMA
         for (int t = lane; t < a.d; t += 64)
             qv[t] = a.x[(int64_t)q * a.d + t];
@@ -374,6 +396,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
         }
         __syncthreads();
 
+        DRM_STAMP(0);
         // --- greedy_update_nearest on levels max_level .. 1
         int32_t nearest = a.entry_point;
         uint32_t dn = ufirst(ord32(pq_distance_code<FAST8>(a, lut, nearest, load_code8<FAST8>(a, nearest))));
@@ -407,6 +430,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
         }
         const int nhops_upper = nhops;
 
+        DRM_STAMP(1);
         // --- level 0. Result handler: k slots of (+inf,-1) (HeapBlockResultHandler::begin)
         uint32_t rk[R], ri[R], ck[R], ci[R];
 #pragma unroll
@@ -459,7 +483,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             hcount = 1;
         } else {
             if (lane == 0) {
-                atomicOr(&vis[nearest >> 5], 1u << (nearest & 31));
+                vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
                 if (a.clear_cap > 0)
                     clr[0] = nearest;
             }
@@ -498,6 +522,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             if (below >= a.efSearch)
                 break;
 
+            DRM_STAMP(2);
             // expand v0's level-0 row (one coalesced 128-B load at M_hnsw = 16)
             const int32_t v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
             const uint64_t negm = __ballot(lane < a.deg0 && v1 < 0);
@@ -513,7 +538,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                     const bool has = hv >= 0;
                     const uint64_t m = __ballot(has);
                     if (has) {
-                        atomicOr(&vis[hv >> 5], 1u << (hv & 31));
+                        vis_test_set(&vis[hv >> 5], 1u << (hv & 31));
                         const int p = clear_n + __popcll(m & lanes_below(lane));
                         if (p < a.clear_cap)
                             clr[p] = hv;
@@ -538,7 +563,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                     }
                 } else {
                     const uint32_t bit = 1u << (v1 & 31);
-                    const uint32_t old = atomicOr(&vis[v1 >> 5], bit);
+                    const uint32_t old = vis_test_set(&vis[v1 >> 5], bit);
                     fresh = (old & bit) == 0u;
                 }
             }
@@ -549,6 +574,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                         fresh = false;
                 }
             }
+            DRM_STAMP(3);
             const uint64_t fm = __ballot(fresh);
             const int nf = __popcll(fm);
             if (spilled && fresh) {
@@ -567,6 +593,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                 dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
             }
             ndis0 += nf;
+            DRM_STAMP(4);
             // add_to_heap for each fresh link in row order (wave-uniform scalar loop)
             uint64_t rem = fm;
             while (rem) {
@@ -594,8 +621,10 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                 ++nvalid;
             }
             nstep++;
+            DRM_STAMP(5);
         }
 
+        DRM_STAMP(2);
         // --- SingleResultHandler::end (heap_reorder): the sorted slots are already its output
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -626,7 +655,11 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
+        DRM_STAMP(6);
     }
+    if (STAMPS && lane_id() == 0 && a.stamps)
+        for (int i = 0; i < 8; ++i)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
 } // namespace
@@ -722,6 +755,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.clear_cap = ix.clear_cap;
     a.counter = ix.counter;
     a.check_dups = ix.has_dup_links;
+    a.stamps = ix.stamps;
 
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, sizeof(uint32_t), stream));
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
@@ -735,7 +769,9 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     case 3: case 4: DRM_LAUNCH(4, F8, VM, SP); break;                                                           \
     default: DRM_LAUNCH(8, F8, VM, SP); break;                                                                  \
     }
-    if (fast8) {
+    if (fast8 && ix.stamps && R == 2 && vmode == 0 && spec) {
+        hipLaunchKernelGGL((hnsw_pq_search_kernel<2, true, 0, true, true>), dim3(slots), dim3(64), lds, stream, a);
+    } else if (fast8) {
         if (vmode == 1) {
             if (spec) { DRM_LAUNCH_R(true, 1, true) } else { DRM_LAUNCH_R(true, 1, false) }
         } else {

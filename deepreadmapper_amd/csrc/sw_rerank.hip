@@ -48,6 +48,57 @@ __device__ __forceinline__ void sw_row(int (&H)[LQ], const uint32_t (&bv)[(LQ + 
     }
 }
 
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// Two candidates per lane in 16-bit halves (lo = candidate a, hi = candidate b). pw[g] carries the
+// match bits of query positions 8g..8g+7 for both candidates (bit 2t+1 of each half), so one 32-bit
+// shift + mask yields 2*match for both; scores <= 256 never carry across halves.
+template <int LQ>
+__device__ __forceinline__ void sw_row_pk(uint32_t (&H)[LQ], const uint32_t (&pw)[(LQ + 7) / 8], us2 &best)
+{
+    uint32_t t_next = pw[0] & 0x00020002u; // diag of column 0 is the zero border
+    us2 left = {0, 0};
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+        const uint32_t t = t_next;
+        const uint32_t up = H[j];
+        if (j + 1 < LQ)
+            t_next = up + ((pw[(j + 1) >> 3] >> (2 * ((j + 1) & 7))) & 0x00020002u);
+        us2 h = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(us2, t),
+                                                                    __builtin_bit_cast(us2, up)),
+                                          left);
+        h = __builtin_elementwise_sub_sat(h, (us2){1, 1});
+        H[j] = __builtin_bit_cast(uint32_t, h);
+        left = h;
+        best = __builtin_elementwise_max(best, h);
+    }
+}
+
+// Interleave the profile rows of two candidate bytes into pw (see sw_row_pk).
+template <int LQ>
+__device__ __forceinline__ void load_profile_pk(const uint32_t *prof, int ca, int cb, uint32_t (&pw)[(LQ + 7) / 8])
+{
+    constexpr int NW = (LQ + 15) / 16;
+    constexpr int NWP = (NW + 3) & ~3;
+    constexpr int NG = (LQ + 7) / 8;
+    const uint4 *pa = reinterpret_cast<const uint4 *>(prof + (size_t)ca * NWP);
+    const uint4 *pb = reinterpret_cast<const uint4 *>(prof + (size_t)cb * NWP);
+#pragma unroll
+    for (int w4 = 0; w4 < NWP / 4; ++w4) {
+        const uint4 va = pa[w4], vb = pb[w4];
+        const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
+        const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int w = w4 * 4 + e;
+            if (2 * w < NG)
+                pw[2 * w] = __builtin_amdgcn_perm(wb[e], wa[e], 0x05040100u);
+            if (2 * w + 1 < NG)
+                pw[2 * w + 1] = __builtin_amdgcn_perm(wb[e], wa[e], 0x07060302u);
+        }
+    }
+}
+
 template <int LQ>
 __device__ __forceinline__ void load_profile(const uint32_t *prof, int ch, uint32_t (&bv)[(LQ + 15) / 16])
 {
@@ -142,37 +193,37 @@ __device__ void ps_partial_sort(uint32_t *e, int n, int k)
 }
 
 // Kernel 1 of the rerank: candidate lists (find_sequences static) + one SW score per candidate.
-// One 128-thread workgroup per query (grid-stride); lane = candidate.
+// One 64-lane workgroup per query (grid-stride); each lane scores two candidates (16-bit halves).
 template <int LQ>
-__global__ __launch_bounds__(128) void sw_score_kernel(RerankArgs a)
+__global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
 {
     constexpr int NW = (LQ + 15) / 16;
     constexpr int NWP = (NW + 3) & ~3;
     __shared__ __align__(16) uint32_t prof[257 * NWP];
     __shared__ __align__(16) uint8_t qbuf[LQ];
     __shared__ uint64_t cand[kMaxCands];
-    __shared__ int wave_cnt[2];
     __shared__ int ncand_s;
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x; // one wave per workgroup
+    const int lane = tid & 63;
     for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
         const int qlen = a.q_len[q];
         const int nsel = min(a.k_clusters, a.kk);
         const int64_t *nb = a.neighbors + q * a.kk;
-        if (a.stride == 1 && nsel <= 128) {
+        if (a.stride == 1 && nsel <= kMaxCands) {
             // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
-            const uint64_t id = (tid < nsel) ? (uint64_t)nb[tid] : ~0ull;
-            const bool keep = id < (uint64_t)a.n_ref;
-            const uint64_t m = __ballot(keep);
-            if (lane == 0)
-                wave_cnt[wv] = __popcll(m);
-            __syncthreads();
-            const int base = (wv == 1) ? wave_cnt[0] : 0;
-            if (keep)
-                cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = id;
+            int base = 0;
+            for (int c = 0; c < nsel; c += 64) {
+                const int i = c + lane;
+                const uint64_t id = (i < nsel) ? (uint64_t)nb[i] : ~0ull;
+                const bool keep = id < (uint64_t)a.n_ref;
+                const uint64_t m = __ballot(keep);
+                if (keep)
+                    cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = id;
+                base += __popcll(m);
+            }
             if (tid == 0)
-                ncand_s = wave_cnt[0] + wave_cnt[1];
+                ncand_s = base;
         } else if (tid == 0) {
             // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride), duplicates kept
             int nc = 0;
@@ -212,26 +263,37 @@ __global__ __launch_bounds__(128) void sw_score_kernel(RerankArgs a)
         const int ncand = (qlen > LQ) ? -3 : ncand_s;
         if (tid == 0)
             a.ncand[q] = ncand;
-        for (int c = tid; c < ncand; c += blockDim.x) {
-            int H[LQ];
+        // two candidates per lane: c and c + blockDim.x
+        for (int c0 = tid; c0 < ncand; c0 += 2 * blockDim.x) {
+            const int c1 = c0 + (int)blockDim.x;
+            const bool has_b = c1 < ncand;
+            uint32_t H[LQ];
 #pragma unroll
             for (int j = 0; j < LQ; ++j)
-                H[j] = 0;
-            int best = 0;
-            const uint64_t wid = cand[c];
-            const uint8_t *win = a.refs + (size_t)wid * (size_t)a.row_stride;
+                H[j] = 0u;
+            us2 best = {0, 0};
+            const uint64_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
+            const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
+            const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
             const int L = a.ref_len;
-            int ch_next = (L > 0) ? (int)win[0] : kPadRow;
+            int na = (L > 0) ? (int)pa[0] : kPadRow;
+            int nb2 = (L > 0 && has_b) ? (int)pb[0] : kPadRow;
             for (int i = 0; i < L; ++i) {
-                const int ch = ch_next;
-                if (i + 1 < L)
-                    ch_next = win[i + 1]; // prefetch the next row's byte
-                uint32_t bv[NW];
-                load_profile<LQ>(prof, ch, bv);
-                sw_row<LQ>(H, bv, best);
+                const int ca = na, cb = nb2;
+                if (i + 1 < L) { // prefetch the next row's bytes
+                    na = pa[i + 1];
+                    nb2 = has_b ? (int)pb[i + 1] : kPadRow;
+                }
+                uint32_t pw[(LQ + 7) / 8];
+                load_profile_pk<LQ>(prof, ca, cb, pw);
+                sw_row_pk<LQ>(H, pw, best);
             }
-            a.cand_ids[q * a.cmax + c] = wid;
-            a.cand_scores[q * a.cmax + c] = best;
+            a.cand_ids[q * a.cmax + c0] = wa;
+            a.cand_scores[q * a.cmax + c0] = (int32_t)best.x;
+            if (has_b) {
+                a.cand_ids[q * a.cmax + c1] = wb;
+                a.cand_scores[q * a.cmax + c1] = (int32_t)best.y;
+            }
         }
         __syncthreads();
     }
@@ -360,13 +422,13 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     const int grid = (int)std::min<int64_t>(a.nq, 65536);
     switch (pick_lq(max_qlen)) {
     case 64:
-        hipLaunchKernelGGL(sw_score_kernel<64>, dim3(grid), dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(sw_score_kernel<64>, dim3(grid), dim3(64), 0, stream, a);
         break;
     case 152:
-        hipLaunchKernelGGL(sw_score_kernel<152>, dim3(grid), dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(sw_score_kernel<152>, dim3(grid), dim3(64), 0, stream, a);
         break;
     default:
-        hipLaunchKernelGGL(sw_score_kernel<256>, dim3(grid), dim3(128), 0, stream, a);
+        hipLaunchKernelGGL(sw_score_kernel<256>, dim3(grid), dim3(64), 0, stream, a);
         break;
     }
     DRM_HIP_CHECK(hipGetLastError());

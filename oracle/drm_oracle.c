@@ -229,6 +229,8 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
  * faiss IndexHNSWPQ search [upstream faiss >= 1.8].
  * ====================================================================================== */
 
+/* operation counters (diagnostic; summed over all queries of the last oracle_hnswpq_search call) */
+static int64_t g_cnt_push, g_cnt_pop, g_cnt_reject, g_cnt_result;
 /* faiss::CMax<T,TI>::cmp2 -- (a1 > b1) || (a1 == b1 && a2 > b2) */
 #define CMP2(v1, v2, i1, i2) (((v1) > (v2)) || (((v1) == (v2)) && ((i1) > (i2))))
 
@@ -372,14 +374,21 @@ typedef struct {
 static void mm_push(minimax_t *h, int32_t i, float v)
 {
     if (h->k == h->n) {
-        if (v >= h->dis[0])
+        if (v >= h->dis[0]) {
+#pragma omp atomic
+            g_cnt_reject++;
             return;
+        }
+#pragma omp atomic
+        g_cnt_pop++;
         if (h->ids[0] != -1)
             --h->nvalid;
         heap_pop_i32((size_t)h->k--, h->dis, h->ids);
     }
     heap_push_i32((size_t)++h->k, h->dis, h->ids, v, i);
     ++h->nvalid;
+#pragma omp atomic
+    g_cnt_push++;
 }
 
 /* pop_min: minimum dis among valid slots, ties -> highest slot index (the scalar version scans
@@ -463,6 +472,14 @@ static inline float pq_dis(const oracle_hnswpq_t *ix, const float *lut, int64_t 
     for (int m = 0; m < ix->pq_M; ++m)
         r = r + lut[(size_t)m * ix->ksub + pq_decode(code, m, ix->pq_nbits)];
     return r;
+}
+
+void oracle_hnsw_counters(int64_t *out4)
+{
+    out4[0] = g_cnt_push;
+    out4[1] = g_cnt_pop;
+    out4[2] = g_cnt_reject;
+    out4[3] = g_cnt_result;
 }
 
 typedef struct {
@@ -561,6 +578,8 @@ static void hnsw_search_one(const oracle_hnswpq_t *ix, const float *x, int k, in
             ndis += 1;
             /* add_to_heap */
             if (dis < threshold) {
+#pragma omp atomic
+                g_cnt_result++;
                 heap_replace_top_i64((size_t)k, D, I, dis, v1);
                 threshold = D[0];
             }
@@ -587,6 +606,7 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
 {
     if (k <= 0)
         return -1;
+    g_cnt_push = g_cnt_pop = g_cnt_reject = g_cnt_result = 0;
     const int ef = efSearch > k ? efSearch : k;
 #ifdef _OPENMP
     if (nthreads <= 0)

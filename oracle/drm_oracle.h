@@ -66,6 +66,9 @@ void oracle_pq_distance_table(const oracle_hnswpq_t *ix, const float *x, float *
 int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, int k, int efSearch,
                          float *D, int64_t *I, int32_t *ndis, int32_t *nhops, int nthreads);
 
+/* diagnostic: {candidate pushes, pops on full heap, rejected pushes, result insertions} of the last search */
+void oracle_hnsw_counters(int64_t *out4);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,30 @@
+"""Diagnostic: section time shares of the search kernel (stamped build, DRM_SEARCH_STAMPS=1).
+Run on the GPU box after the bench cache exists: DRM_SEARCH_STAMPS=1 python tools/scripts/stamps.py"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from deepreadmapper_amd import synth  # noqa: E402
+from deepreadmapper_amd.device import DeviceBuffer, synchronize  # noqa: E402
+from deepreadmapper_amd.search import HnswPqIndex  # noqa: E402
+from deepreadmapper_amd._native import lib, check  # noqa: E402
+
+w = synth.Workload("c3", 500_149, 100_000, seed=42, read_seed=7).generate("/tmp/drm_bench_cache")
+ix = HnswPqIndex(w.index_path)
+Q = 100_000
+dq = DeviceBuffer.from_host(w.q_emb[:Q])
+dD, dI = DeviceBuffer((Q, 128), np.float32), DeviceBuffer((Q, 128), np.int64)
+ix.search_device(dq, Q, 128, 128, dD, dI)
+synchronize()
+out = np.zeros(8, dtype=np.uint64)
+L = lib()
+L.drm_debug_search_stamps.argtypes = [C.c_void_p, C.c_void_p]
+check(L.drm_debug_search_stamps(ix.handle, out.ctypes.data))
+names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances(LUT sum)",
+         "add_to_heap loop", "output+clear", "queue/top"]
+tot = float(out.sum())
+for n, v in zip(names, out):
+    print(f"{n:28s} {v / tot * 100:6.2f} %")
