@@ -108,12 +108,15 @@ def main():
 
     D = Dist()
     from deepreadmapper_amd import synth
-    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream, set_device, synchronize
+    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream, device_count, set_device, synchronize
+    from deepreadmapper_amd.shard import shard_range
     from deepreadmapper_amd.search import HnswPqIndex
     from deepreadmapper_amd.rerank import WindowTable
     from deepreadmapper_amd._native import check, lib
 
-    set_device(D.local_rank)
+    ndev = device_count()
+    dev = D.local_rank % max(ndev, 1)  # one rank per GPU; ranks share GPUs only on smaller boxes
+    set_device(dev)
     N, Q, K, EF = D.world, args.queries, args.k, args.ef
     w = synth.Workload("c3", 500_149, N * Q, seed=42, read_seed=7)
     # rank 0 builds the shared index file; the others wait, then every rank loads its own replica
@@ -124,13 +127,13 @@ def main():
     D.barrier()
     if D.rank != 0:
         w.generate(args.cache)
-    lo, hi = D.rank * Q, (D.rank + 1) * Q
+    lo, hi = shard_range(N * Q, D.rank, N)  # contiguous query shard of this rank
     q_emb = np.ascontiguousarray(w.q_emb[lo:hi])
     queries = np.ascontiguousarray(w.queries[lo:hi])
     truth = w.truth[lo:hi]
 
-    ix = HnswPqIndex(w.index_path, D.local_rank)
-    table = WindowTable(w.refs, D.local_rank)
+    ix = HnswPqIndex(w.index_path, dev)
+    table = WindowTable(w.refs, dev)
     d_x = DeviceBuffer.from_host(q_emb)
     d_q = DeviceBuffer.from_host(queries)
     d_ql = DeviceBuffer.from_host(np.full(Q, queries.shape[1], dtype=np.int32))

@@ -238,18 +238,17 @@ template <int R> __device__ void heap_pop_par(uint32_t (&hk)[R], uint32_t (&hi)[
     const uint32_t k1 = fetch(hk, s1), k2 = fetch(hk, s2);
     const int32_t i1 = (int32_t)fetch(hi, s1), i2 = (int32_t)fetch(hi, s2);
     const uint64_t lm = __ballot((c2 == k + 1) || cmp2(k1, k2, i1, i2)); // bit p-1: take left child
-    int pl = 1;
-    bool exists = true;
-    for (int t = 0; t < 12; ++t) {
-        if (t >= lane)
+    // uniform walk of the max-child path; lane l receives the position at depth l
+    int pl = 1, depth = 0, mypos = 1;
+    for (int l = 1; l < 12; ++l) {
+        if (2 * pl > k)
             break;
-        if (2 * pl > k) {
-            exists = false;
-            break;
-        }
         pl = 2 * pl + (int)(((lm >> (pl - 1)) & 1ull) ^ 1ull);
+        depth = l;
+        mypos = (lane == l) ? pl : mypos;
     }
-    const bool onpath = lane < 12 && exists;
+    const bool onpath = lane <= depth;
+    pl = mypos;
     const int src = onpath ? pl - 1 : 0;
     const uint32_t ak = fetch(hk, src);
     const int32_t ai = (int32_t)fetch(hi, src);
@@ -614,10 +613,22 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                     kc--;
                 }
                 kc++;
-                if (R <= 2)
-                    heap_push_par(ck, ci, kc, key, id);
-                else
+                if (R <= 2) {
+                    // most pushes stay at the bottom: test the parent with one uniform read first
+                    bool moves = false;
+                    if (kc > 1) {
+                        const int par = (kc >> 1) - 1;
+                        moves = cmp2(key, rd(ck, par), id, (int32_t)rd(ci, par));
+                    }
+                    if (moves) {
+                        heap_push_par(ck, ci, kc, key, id);
+                    } else {
+                        wr(ck, kc - 1, key);
+                        wr(ci, kc - 1, (uint32_t)id);
+                    }
+                } else {
                     heap_push(ck, ci, kc, key, id);
+                }
                 ++nvalid;
             }
             nstep++;

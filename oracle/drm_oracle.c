@@ -231,6 +231,8 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
 
 /* operation counters (diagnostic; summed over all queries of the last oracle_hnswpq_search call) */
 static int64_t g_cnt_push, g_cnt_pop, g_cnt_reject, g_cnt_result;
+/* per-thread tallies, folded into the globals once per thread (no atomics in the hot loop) */
+static _Thread_local int64_t t_push, t_pop, t_reject, t_result;
 /* faiss::CMax<T,TI>::cmp2 -- (a1 > b1) || (a1 == b1 && a2 > b2) */
 #define CMP2(v1, v2, i1, i2) (((v1) > (v2)) || (((v1) == (v2)) && ((i1) > (i2))))
 
@@ -375,20 +377,17 @@ static void mm_push(minimax_t *h, int32_t i, float v)
 {
     if (h->k == h->n) {
         if (v >= h->dis[0]) {
-#pragma omp atomic
-            g_cnt_reject++;
+            t_reject++;
             return;
         }
-#pragma omp atomic
-        g_cnt_pop++;
+        t_pop++;
         if (h->ids[0] != -1)
             --h->nvalid;
         heap_pop_i32((size_t)h->k--, h->dis, h->ids);
     }
     heap_push_i32((size_t)++h->k, h->dis, h->ids, v, i);
     ++h->nvalid;
-#pragma omp atomic
-    g_cnt_push++;
+    t_push++;
 }
 
 /* pop_min: minimum dis among valid slots, ties -> highest slot index (the scalar version scans
@@ -578,8 +577,7 @@ static void hnsw_search_one(const oracle_hnswpq_t *ix, const float *x, int k, in
             ndis += 1;
             /* add_to_heap */
             if (dis < threshold) {
-#pragma omp atomic
-                g_cnt_result++;
+                t_result++;
                 heap_replace_top_i64((size_t)k, D, I, dis, v1);
                 threshold = D[0];
             }
@@ -620,11 +618,21 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
         s.visno = 1;
         s.cand.ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)ef);
         s.cand.dis = (float *)malloc(sizeof(float) * (size_t)ef);
+        t_push = t_pop = t_reject = t_result = 0;
 #ifdef _OPENMP
 #pragma omp for schedule(guided)
 #endif
         for (int64_t i = 0; i < n; ++i)
             hnsw_search_one(ix, x + i * ix->d, k, efSearch, D + i * k, I + i * k, ndis + i, nhops + i, &s);
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            g_cnt_push += t_push;
+            g_cnt_pop += t_pop;
+            g_cnt_reject += t_reject;
+            g_cnt_result += t_result;
+        }
         free(s.lut);
         free(s.visited);
         free(s.cand.ids);
