@@ -173,6 +173,7 @@ def main():
     sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
 
     # correctness / quality of this rank's last step
+    n_fallback = ix.fallbacks()
     st = d_st.download()
     if not (st == K).all():
         raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")
@@ -219,6 +220,7 @@ def main():
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
                           "bytes_per_query": round(float(bytes_q.mean()), 1),
+                          "tie_fallback_queries": n_fallback,
                           "truth_top1": round(top1, 4), "truth_in_topk": round(intop, 4)},
         }
         print(json.dumps(result), flush=True)

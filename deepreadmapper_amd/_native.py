@@ -24,7 +24,7 @@ EXPORTS = [
     "drm_free", "drm_memset", "drm_memcpy_h2d", "drm_memcpy_d2h", "drm_stream_create", "drm_stream_destroy",
     "drm_stream_sync", "drm_event_create", "drm_event_destroy", "drm_event_record", "drm_event_elapsed_ms",
     "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device",
-    "drm_search_device_ex", "drm_sw_scores",
+    "drm_search_device_ex", "drm_search_fallbacks", "drm_sw_scores",
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
     "drm_build_hnswpq", "drm_embed_kmer3",
 ]
@@ -85,6 +85,7 @@ def lib():
         "drm_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "drm_search_device_ex": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),
+        "drm_search_fallbacks": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_sw_scores": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "drm_refs_create": (C.c_int, [vp, i64, i32, i64, C.c_int, C.POINTER(vp)]),
         "drm_refs_free": (C.c_int, [vp]),

@@ -74,7 +74,8 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 
 void free_index(drm::DeviceIndex &d)
 {
-    void *ptrs[] = {d.centroids, d.codes, d.nbr0, d.upper_off, d.upper_nbr, d.visited, d.clear_list, d.counter, d.stamps};
+    void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr,
+                    d.visited,   d.clear_list, d.counter, d.stamps,   d.fb_list};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -217,11 +218,11 @@ int drm_index_load(const char *path, int device, drm_index **out)
             }
         }
         d.upper_len = (int64_t)upper.size();
-        // tuning knobs: visited-set placement, speculative code loads, kernel choice
+        // tuning knobs: visited-set placement, kernel choice
         if (const char *e = std::getenv("DRM_SEARCH_VMODE"))
             d.vmode = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_SPEC"))
-            d.spec_codes = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_EXACT"))
+            d.force_exact = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
             d.force_lds_kernel = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
@@ -271,6 +272,20 @@ int drm_debug_search_stamps(drm_index *index, uint64_t *out8)
             throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
         DRM_HIP_CHECK(hipMemcpy(out8, index->dev.stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
         DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 8 * sizeof(uint64_t)));
+    });
+}
+
+int drm_search_fallbacks(drm_index *index, int64_t *count)
+{
+    return guarded([&] {
+        if (!index || !count)
+            throw Error(DRM_ERR_ARG, "null argument");
+        uint32_t c[2] = {0, 0};
+        if (index->dev.counter) {
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+        }
+        *count = (int64_t)c[1];
     });
 }
 

@@ -28,7 +28,7 @@ struct DeviceIndex {
     int32_t cum[kMaxLevels + 1] = {};
     int32_t has_dup_links = 0; // some neighbour row lists one id twice
     int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
-    int32_t spec_codes = 1;    // issue PQ code loads before the visited test
+    int32_t force_exact = 0;   // skip the sorted-array pass (every query through the exact kernel)
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
@@ -43,7 +43,9 @@ struct DeviceIndex {
     uint32_t *visited = nullptr;   // [n_slots][vis_words]
     int32_t clear_cap = 0;
     int32_t *clear_list = nullptr; // [n_slots][clear_cap]
-    uint32_t *counter = nullptr;   // work queue head
+    uint32_t *counter = nullptr;   // [0] work queue head, [1] fallback count, [2] fallback queue head
+    int32_t *fb_list = nullptr;    // queries the sorted-array pass handed to the exact kernel
+    int64_t fb_cap = 0;
     int64_t device_bytes = 0;
     HnswPqHost meta; // header fields kept for drm_index_get_info (vectors released)
 };
@@ -74,6 +76,10 @@ struct SearchArgs {
     uint32_t *counter;
     int32_t check_dups;
     uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1), else null
+    const int32_t *qlist;  // exact kernel, fallback pass: process qlist[0 .. *qcount) instead of 0 .. n
+    const uint32_t *qcount;
+    int32_t *fb_list;      // sorted-array kernel: queries handed to the exact kernel
+    uint32_t *fb_count;
 };
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,

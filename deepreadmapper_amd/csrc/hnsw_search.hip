@@ -238,17 +238,15 @@ template <int R> __device__ void heap_pop_par(uint32_t (&hk)[R], uint32_t (&hi)[
     const uint32_t k1 = fetch(hk, s1), k2 = fetch(hk, s2);
     const int32_t i1 = (int32_t)fetch(hi, s1), i2 = (int32_t)fetch(hi, s2);
     const uint64_t lm = __ballot((c2 == k + 1) || cmp2(k1, k2, i1, i2)); // bit p-1: take left child
-    // uniform walk of the max-child path; lane l receives the position at depth l
-    int pl = 1, depth = 0, mypos = 1;
-    for (int l = 1; l < 12; ++l) {
-        if (2 * pl > k)
-            break;
-        pl = 2 * pl + (int)(((lm >> (pl - 1)) & 1ull) ^ 1ull);
-        depth = l;
-        mypos = (lane == l) ? pl : mypos;
+    // uniform (scalar) walk of the max-child path down to its last node `leaf` at depth `depth`;
+    // the path node at depth l is the leaf's ancestor leaf >> (depth - l)
+    int leaf = 1, depth = 0;
+    while (2 * leaf <= k) {
+        leaf = 2 * leaf + (int)(((lm >> (leaf - 1)) & 1ull) ^ 1ull);
+        ++depth;
     }
     const bool onpath = lane <= depth;
-    pl = mypos;
+    const int pl = onpath ? (leaf >> (depth - lane)) : 0;
     const int src = onpath ? pl - 1 : 0;
     const uint32_t ak = fetch(hk, src);
     const int32_t ai = (int32_t)fetch(hi, src);
@@ -258,8 +256,7 @@ template <int R> __device__ void heap_pop_par(uint32_t (&hk)[R], uint32_t (&hi)[
     for (int r = 0; r < R; ++r) {
         const int pos = lane + 64 * r + 1;
         const int m = 31 - __builtin_clz((unsigned)pos);
-        const int pm = __shfl(pl, m & 63, 64);
-        const bool on = m <= h && pm == pos;
+        const bool on = m <= h && (leaf >> (depth - m)) == pos;
         const int srcl = (m + 1) & 63;
         const uint32_t vk = (uint32_t)__shfl((int)ak, srcl, 64);
         const int32_t vi = __shfl(ai, srcl, 64);
@@ -311,6 +308,103 @@ template <bool FAST8> __device__ __forceinline__ uint2 load_code8(const SearchAr
     return make_uint2(0u, 0u);
 }
 
+// set_query: qv <- x[q], LUT[m][c] = sum_t (x - c)^2 over the sub-vector, sequential t, no FMA
+// (PQDistanceComputer::set_query -> compute_distance_table) [upstream faiss]
+__device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float *lut, float *qv, int lane)
+{
+    for (int t = lane; t < a.d; t += 64)
+        qv[t] = a.x[(int64_t)q * a.d + t];
+    __syncthreads();
+    if (a.dsub == 16 && (a.ksub & 127) == 0) {
+        // 2 entries of one sub-quantizer per lane per pass, 8 float4 loads in flight
+        for (int e0 = lane; e0 < a.M * a.ksub; e0 += 128) {
+            const int m = e0 / a.ksub;
+            const float4 *xs = reinterpret_cast<const float4 *>(qv + m * 16);
+            float4 c[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float4 *cp = reinterpret_cast<const float4 *>(a.centroids + (size_t)(e0 + 64 * u) * 16);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    c[u][i] = cp[i];
+            }
+            float acc[2] = {0.0f, 0.0f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float4 x = xs[i];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    float df = __fsub_rn(x.x, c[u][i].x);
+                    acc[u] = __fadd_rn(acc[u], __fmul_rn(df, df));
+                    df = __fsub_rn(x.y, c[u][i].y);
+                    acc[u] = __fadd_rn(acc[u], __fmul_rn(df, df));
+                    df = __fsub_rn(x.z, c[u][i].z);
+                    acc[u] = __fadd_rn(acc[u], __fmul_rn(df, df));
+                    df = __fsub_rn(x.w, c[u][i].w);
+                    acc[u] = __fadd_rn(acc[u], __fmul_rn(df, df));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                lut[e0 + 64 * u] = acc[u];
+        }
+    } else
+    for (int e = lane; e < a.M * a.ksub; e += 64) {
+        const int m = e / a.ksub;
+        const float *cen = a.centroids + (size_t)e * a.dsub;
+        const float *xs = qv + m * a.dsub;
+        float acc = 0.0f;
+        for (int t = 0; t < a.dsub; ++t) {
+            const float diff = __fsub_rn(xs[t], cen[t]);
+            acc = __fadd_rn(acc, __fmul_rn(diff, diff));
+        }
+        lut[e] = acc;
+    }
+    __syncthreads();
+
+}
+
+// greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss]
+template <bool FAST8>
+__device__ __forceinline__ void greedy_upper(const SearchArgs &a, const float *lut, int lane, int32_t &nearest_out,
+                                             uint32_t &dn_out, int &ndis_out, int &nhops_out)
+{
+    int32_t nearest = a.entry_point;
+    uint32_t dn = ufirst(ord32(pq_distance_code<FAST8>(a, lut, nearest, load_code8<FAST8>(a, nearest))));
+    int ndis = 0, nhops = 0;
+    for (int level = a.max_level; level >= 1; --level) {
+        const int cnt = a.cum[level + 1] - a.cum[level];
+        for (;;) {
+            const int32_t prev = nearest;
+            const uint32_t base = a.upper_off[nearest] + (uint32_t)(a.cum[level] - a.cum[1]);
+            const int32_t v = (lane < cnt) ? a.upper_nbr[base + lane] : -1;
+            const uint64_t neg = __ballot(lane < cnt && v < 0);
+            const int nvalid = neg ? (__ffsll((unsigned long long)neg) - 1) : cnt;
+            uint32_t dk = 0xFFFFFFFFu;
+            if (lane < nvalid)
+                dk = ord32(pq_distance_code<FAST8>(a, lut, v, load_code8<FAST8>(a, v)));
+            ndis += nvalid;
+            nhops += 1;
+            // sequential `if (dis < d_nearest)` in link order == first lane holding the minimum
+            uint64_t key = (lane < nvalid) ? (((uint64_t)dk << 32) | (uint32_t)lane) : ~0ull;
+            key = wave_min_u64(key);
+            if (key != ~0ull) {
+                const uint32_t bk = (uint32_t)(key >> 32);
+                if (bk < dn) {
+                    dn = bk;
+                    nearest = __builtin_amdgcn_readlane(v, (int)(key & 63));
+                }
+            }
+            if (nearest == prev)
+                break;
+        }
+    }
+    nearest_out = nearest;
+    dn_out = dn;
+    ndis_out = ndis;
+    nhops_out = nhops;
+}
+
 // Each bitmap slot is owned by exactly one workgroup (one wave) for the whole launch, so a
 // workgroup-scope atomic is sufficient: it is performed in the XCD's L2 instead of memory-side.
 __device__ __forceinline__ uint32_t vis_test_set(uint32_t *w, uint32_t bit)
@@ -338,7 +432,7 @@ __device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9
     } while (0)
 
 template <int R, bool FAST8, int VMODE, bool SPEC, bool STAMPS = false>
-__global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hnsw_pq_search_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -350,14 +444,18 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     const uint32_t kInfKey = ord32(INFINITY);
+    // queue: 0..n-1, or (fallback pass) the *qcount query ids in qlist
+    const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
 
     for (;;) {
         int q = 0;
         if (lane == 0)
             q = (int)atomicAdd(a.counter, 1u);
         q = __builtin_amdgcn_readfirstlane(q);
-        if ((int64_t)q >= a.n)
+        if ((int64_t)q >= nq)
             break;
+        if (a.qlist)
+            q = __builtin_amdgcn_readfirstlane(a.qlist[q]);
 
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < a.k; j += 64) {
@@ -373,60 +471,18 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             continue;
         }
         DRM_STAMP(7);
-        // --- set_query: LUT[m][c] = sum_t (x - c)^2, sequential t, no FMA
-        for (int t = lane; t < a.d; t += 64)
-            qv[t] = a.x[(int64_t)q * a.d + t];
+        // --- set_query
         if (VMODE == 1) {
             int4 *h4 = reinterpret_cast<int4 *>(ht);
             for (int t = lane; t < kHashSlots / 4; t += 64)
                 h4[t] = make_int4(-1, -1, -1, -1);
         }
-        __syncthreads();
-        for (int e = lane; e < a.M * a.ksub; e += 64) {
-            const int m = e / a.ksub;
-            const float *cen = a.centroids + (size_t)e * a.dsub;
-            const float *xs = qv + m * a.dsub;
-            float acc = 0.0f;
-            for (int t = 0; t < a.dsub; ++t) {
-                const float diff = __fsub_rn(xs[t], cen[t]);
-                acc = __fadd_rn(acc, __fmul_rn(diff, diff));
-            }
-            lut[e] = acc;
-        }
-        __syncthreads();
-
+        build_lut(a, q, lut, qv, lane);
         DRM_STAMP(0);
-        // --- greedy_update_nearest on levels max_level .. 1
-        int32_t nearest = a.entry_point;
-        uint32_t dn = ufirst(ord32(pq_distance_code<FAST8>(a, lut, nearest, load_code8<FAST8>(a, nearest))));
-        int ndis = 0, nhops = 0;
-        for (int level = a.max_level; level >= 1; --level) {
-            const int cnt = a.cum[level + 1] - a.cum[level];
-            for (;;) {
-                const int32_t prev = nearest;
-                const uint32_t base = a.upper_off[nearest] + (uint32_t)(a.cum[level] - a.cum[1]);
-                const int32_t v = (lane < cnt) ? a.upper_nbr[base + lane] : -1;
-                const uint64_t neg = __ballot(lane < cnt && v < 0);
-                const int nvalid = neg ? (__ffsll((unsigned long long)neg) - 1) : cnt;
-                uint32_t dk = 0xFFFFFFFFu;
-                if (lane < nvalid)
-                    dk = ord32(pq_distance_code<FAST8>(a, lut, v, load_code8<FAST8>(a, v)));
-                ndis += nvalid;
-                nhops += 1;
-                // sequential `if (dis < d_nearest)` in link order == first lane holding the minimum
-                uint64_t key = (lane < nvalid) ? (((uint64_t)dk << 32) | (uint32_t)lane) : ~0ull;
-                key = wave_min_u64(key);
-                if (key != ~0ull) {
-                    const uint32_t bk = (uint32_t)(key >> 32);
-                    if (bk < dn) {
-                        dn = bk;
-                        nearest = __builtin_amdgcn_readlane(v, (int)(key & 63));
-                    }
-                }
-                if (nearest == prev)
-                    break;
-            }
-        }
+        int32_t nearest;
+        uint32_t dn;
+        int ndis, nhops;
+        greedy_upper<FAST8>(a, lut, lane, nearest, dn, ndis, nhops);
         const int nhops_upper = nhops;
 
         DRM_STAMP(1);
@@ -491,6 +547,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
         __syncthreads();
 
         int nstep = 0, ndis0 = 0;
+        int32_t pred = -1, v1_pref = -1; // row of the node predicted to be popped next, loaded early
         while (nvalid > 0) {
             // pop_min: smallest distance among valid slots, ties -> highest slot
             uint32_t bh = 0xFFFFFFFFu, bl = 0xFFFFFFFFu;
@@ -523,7 +580,9 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
 
             DRM_STAMP(2);
             // expand v0's level-0 row (one coalesced 128-B load at M_hnsw = 16)
-            const int32_t v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
+            int32_t v1 = v1_pref;
+            if (v0 != pred)
+                v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
             const uint64_t negm = __ballot(lane < a.deg0 && v1 < 0);
             const int jmax = negm ? (__ffsll((unsigned long long)negm) - 1) : a.deg0;
             const bool act = lane < jmax;
@@ -576,11 +635,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             DRM_STAMP(3);
             const uint64_t fm = __ballot(fresh);
             const int nf = __popcll(fm);
-            if (spilled && fresh) {
-                const int p = clear_n + __popcll(fm & lanes_below(lane));
-                if (p < a.clear_cap)
-                    clr[p] = v1;
-            }
+            const int clear_base = clear_n;
             if (spilled)
                 clear_n += nf;
             else
@@ -592,6 +647,33 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
                 dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
             }
             ndis0 += nf;
+            {
+                // Predict the next pop_min (smallest valid candidate after this row's pushes) and
+                // start loading its row now, so the load overlaps the heap updates below. A wrong
+                // prediction (ties, evictions) only costs a reload.
+                uint32_t mk = fresh ? dk : 0xFFFFFFFFu;
+                uint32_t mid = (uint32_t)v1;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int s = lane + 64 * r;
+                    if (s < kc && ci[r] != 0xFFFFFFFFu && ck[r] < mk) {
+                        mk = ck[r];
+                        mid = ci[r];
+                    }
+                }
+                const uint32_t m = wave_min_u32(mk);
+                pred = -1;
+                if (m != 0xFFFFFFFFu) {
+                    pred = __builtin_amdgcn_readlane((int)mid, __builtin_ctzll(__ballot(mk == m)));
+                    v1_pref = (lane < a.deg0) ? a.nbr0[(size_t)pred * (size_t)a.deg0 + lane] : -1;
+                }
+            }
+            // clear-list entries are stored after the loads above so that no wait covers them
+            if (spilled && fresh) {
+                const int p = clear_base + __popcll(fm & lanes_below(lane));
+                if (p < a.clear_cap)
+                    clr[p] = v1;
+            }
             DRM_STAMP(4);
             // add_to_heap for each fresh link in row order (wave-uniform scalar loop)
             uint64_t rem = fm;
@@ -673,6 +755,254 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_kernel(SearchArgs a)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Fast path: the MinimaxHeap and the result heap as ONE register-resident array sorted by key.
+//
+// While no two entries of the candidate set share a distance, faiss's behaviour does not depend on
+// the heap's slot layout: pop_min's minimum is unique, the evicted maximum is unique, count_below(d0)
+// is the popped entry's rank, and (k <= ef, same acceptance rule `d < max`) the result heap holds
+// exactly the first k entries of the candidate set. So slot s (lane s & 63, register s >> 6) keeps
+// the s-th smallest (key, id), bit 31 of the id marks a popped entry, pushing is one sorted insert
+// (ballot rank + DPP shift), pop_min is the first unpopped slot and eviction drops the last slot.
+// A query that would insert a distance already present (or +inf) is abandoned and appended to
+// a.fb_list; the exact kernel above re-runs it, so every output is bit-identical to the oracle.
+template <int R, bool FAST8, bool STAMPS = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hnsw_pq_search_sorted_kernel(
+    SearchArgs a)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    const int lane = lane_id();
+    float *lut = reinterpret_cast<float *>(smem);
+    float *qv = lut + a.M * a.ksub;
+    uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
+    int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
+    const uint32_t kInfKey = ord32(INFINITY);
+    constexpr uint32_t kPopped = 0x80000000u;
+
+    for (;;) {
+        int q = 0;
+        if (lane == 0)
+            q = (int)atomicAdd(a.counter, 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if ((int64_t)q >= a.n)
+            break;
+
+        if (a.entry_point < 0 || a.ntotal == 0) {
+            for (int j = lane; j < a.k; j += 64) {
+                a.D[(int64_t)q * a.k + j] = INFINITY;
+                a.I[(int64_t)q * a.k + j] = -1;
+            }
+            if (lane == 0) {
+                a.ndis[q] = 0;
+                a.nhops[q] = 0;
+                if (a.nhops_upper)
+                    a.nhops_upper[q] = 0;
+            }
+            continue;
+        }
+        DRM_STAMP(7);
+        build_lut(a, q, lut, qv, lane);
+        DRM_STAMP(0);
+        int32_t nearest;
+        uint32_t dn;
+        int ndis, nhops;
+        greedy_upper<FAST8>(a, lut, lane, nearest, dn, ndis, nhops);
+        const int nhops_upper = nhops;
+        DRM_STAMP(1);
+
+        // candidate set: unused slots hold (~0, ~0) -- above every key, and "popped"
+        uint32_t ck[R], ci[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ck[r] = 0xFFFFFFFFu;
+            ci[r] = 0xFFFFFFFFu;
+        }
+        wr(ck, 0, dn);
+        wr(ci, 0, (uint32_t)nearest);
+        int kc = 1, nvalid = 1;
+        bool tie = dn == kInfKey; // the result handler would reject +inf, the candidate heap not
+        if (lane == 0) {
+            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
+            if (a.clear_cap > 0)
+                clr[0] = nearest;
+        }
+        int clear_n = 1;
+
+        int nstep = 0, ndis0 = 0;
+        int32_t pred = -1, v1_pref = -1;
+        while (nvalid > 0 && !tie) {
+            // pop_min = first unpopped slot; count_below(d0) = its rank
+            int imin = 64 * R;
+#pragma unroll
+            for (int r = R - 1; r >= 0; --r) {
+                const uint64_t m = __ballot((ci[r] & kPopped) == 0u);
+                if (m)
+                    imin = 64 * r + __builtin_ctzll(m);
+            }
+            const int32_t v0 = (int32_t)rd(ci, imin);
+            wr(ci, imin, (uint32_t)v0 | kPopped);
+            nvalid--;
+            if (imin >= a.efSearch)
+                break;
+
+            DRM_STAMP(2);
+            int32_t v1 = v1_pref;
+            if (v0 != pred)
+                v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
+            const uint64_t negm = __ballot(lane < a.deg0 && v1 < 0);
+            const int jmax = negm ? (__ffsll((unsigned long long)negm) - 1) : a.deg0;
+            const bool act = lane < jmax;
+            uint2 c8 = make_uint2(0u, 0u);
+            if (FAST8 && act)
+                c8 = load_code8<FAST8>(a, v1);
+            bool fresh = false;
+            if (act) {
+                const uint32_t bit = 1u << (v1 & 31);
+                const uint32_t old = vis_test_set(&vis[v1 >> 5], bit);
+                fresh = (old & bit) == 0u;
+            }
+            if (a.check_dups) {
+                for (int j = 0; j < jmax; ++j) {
+                    const int32_t vj = __shfl(v1, j, 64);
+                    if (j < lane && vj == v1)
+                        fresh = false;
+                }
+            }
+            DRM_STAMP(3);
+            const uint64_t fm = __ballot(fresh);
+            const int nf = __popcll(fm);
+            const int clear_base = clear_n;
+            clear_n += nf;
+            uint32_t dk = 0xFFFFFFFFu;
+            if (fresh) {
+                if (!FAST8)
+                    c8 = load_code8<FAST8>(a, v1);
+                dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
+            }
+            ndis0 += nf;
+            {
+                // prefetch the row of the likely next pop_min (a wrong guess only costs a reload)
+                int inext = 64 * R;
+#pragma unroll
+                for (int r = R - 1; r >= 0; --r) {
+                    const uint64_t m = __ballot((ci[r] & kPopped) == 0u);
+                    if (m)
+                        inext = 64 * r + __builtin_ctzll(m);
+                }
+                const uint32_t hk = inext < 64 * R ? rd(ck, inext) : 0xFFFFFFFFu;
+                const uint32_t fmin = wave_min_u32(dk);
+                pred = -1;
+                if (fmin < hk)
+                    pred = __builtin_amdgcn_readlane(v1, __builtin_ctzll(__ballot(dk == fmin)));
+                else if (hk != 0xFFFFFFFFu)
+                    pred = (int32_t)(rd(ci, inext) & ~kPopped);
+                if (pred >= 0)
+                    v1_pref = (lane < a.deg0) ? a.nbr0[(size_t)pred * (size_t)a.deg0 + lane] : -1;
+            }
+            if (fresh) {
+                const int p = clear_base + __popcll(fm & lanes_below(lane));
+                if (p < a.clear_cap)
+                    clr[p] = v1;
+            }
+            DRM_STAMP(4);
+            // push each fresh link in row order
+            uint64_t rem = fm;
+            while (rem) {
+                const int l = __builtin_ctzll(rem);
+                rem &= rem - 1;
+                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
+                const int32_t id = __builtin_amdgcn_readlane(v1, l);
+                const bool full = kc == a.ef;
+                if (full && key >= rd(ck, kc - 1))
+                    continue; // MinimaxHeap::push rejects; the result handler rejects too (k <= ef)
+                int pos = 0;
+                uint64_t eq = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    pos += __popcll(__ballot(ck[r] < key));
+                    eq |= __ballot(ck[r] == key);
+                }
+                if (eq != 0 || key == kInfKey) {
+                    tie = true;
+                    break;
+                }
+                if (full) { // drop the maximum (slot ef-1)
+                    if ((rd(ci, kc - 1) & kPopped) == 0u)
+                        nvalid--;
+                    kc--;
+                }
+                uint32_t pk[R], pi[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t carry_k = r ? (uint32_t)__builtin_amdgcn_readlane((int)ck[r - 1], 63) : 0u;
+                    const uint32_t carry_i = r ? (uint32_t)__builtin_amdgcn_readlane((int)ci[r - 1], 63) : 0u;
+                    pk[r] = wave_shr1(carry_k, ck[r]);
+                    pi[r] = wave_shr1(carry_i, ci[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int s2 = lane + 64 * r;
+                    if (s2 > pos) {
+                        ck[r] = pk[r];
+                        ci[r] = pi[r];
+                    } else if (s2 == pos) {
+                        ck[r] = key;
+                        ci[r] = (uint32_t)id;
+                    }
+                }
+                kc++;
+                nvalid++;
+                if (full && kc < 64 * R) { // the dropped maximum was shifted into slot ef
+                    wr(ck, kc, 0xFFFFFFFFu);
+                    wr(ci, kc, 0xFFFFFFFFu);
+                }
+            }
+            nstep++;
+            DRM_STAMP(5);
+        }
+
+        DRM_STAMP(2);
+        if (tie) { // hand the query to the exact kernel
+            if (lane == 0)
+                a.fb_list[atomicAdd(a.fb_count, 1u)] = q;
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int j = lane + 64 * r;
+                if (j < a.k) {
+                    const int64_t o = (int64_t)q * a.k + j;
+                    const bool valid = j < kc;
+                    a.D[o] = valid ? unord32(ck[r]) : INFINITY;
+                    a.I[o] = valid ? (int64_t)(int32_t)(ci[r] & ~kPopped) : (int64_t)-1;
+                }
+            }
+            if (lane == 0) {
+                a.ndis[q] = ndis + ndis0;
+                a.nhops[q] = nhops + nstep;
+                if (a.nhops_upper)
+                    a.nhops_upper[q] = nhops_upper;
+            }
+        }
+        // VisitedTable::advance
+        if (clear_n <= a.clear_cap) {
+            for (int t = lane; t < clear_n; t += 64)
+                vis[clr[t] >> 5] = 0u;
+        } else {
+            for (int64_t w = lane; w < a.vis_words; w += 64)
+                vis[w] = 0u;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        DRM_STAMP(6);
+    }
+    if (STAMPS && lane_id() == 0 && a.stamps)
+        for (int i = 0; i < 8; ++i)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
+}
+
 } // namespace
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
@@ -729,7 +1059,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
         ix.n_slots = alloc_slots;
     }
     if (!ix.counter)
-        DRM_HIP_CHECK(hipMalloc(&ix.counter, sizeof(uint32_t)));
+        DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
 
     SearchArgs a{};
     a.x = d_x;
@@ -768,31 +1098,55 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.check_dups = ix.has_dup_links;
     a.stamps = ix.stamps;
 
-    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, sizeof(uint32_t), stream));
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
-    const bool spec = ix.spec_codes != 0;
-#define DRM_LAUNCH(RR, F8, VM, SP)                                                                              \
-    hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, SP>), dim3(slots), dim3(64), lds, stream, a)
-#define DRM_LAUNCH_R(F8, VM, SP)                                                                                \
+    const bool sorted_path = !ix.force_exact && vmode == 0 && R <= 2;
+    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 3 * sizeof(uint32_t), stream));
+#define DRM_LAUNCH_EXACT(RR, F8, VM)                                                                           \
+    hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, F8>), dim3(slots), dim3(64), lds, stream, a)
+#define DRM_LAUNCH_EXACT_R(F8, VM)                                                                             \
     switch (R) {                                                                                                \
-    case 1: DRM_LAUNCH(1, F8, VM, SP); break;                                                                   \
-    case 2: DRM_LAUNCH(2, F8, VM, SP); break;                                                                   \
-    case 3: case 4: DRM_LAUNCH(4, F8, VM, SP); break;                                                           \
-    default: DRM_LAUNCH(8, F8, VM, SP); break;                                                                  \
+    case 1: DRM_LAUNCH_EXACT(1, F8, VM); break;                                                                 \
+    case 2: DRM_LAUNCH_EXACT(2, F8, VM); break;                                                                 \
+    case 3: case 4: DRM_LAUNCH_EXACT(4, F8, VM); break;                                                         \
+    default: DRM_LAUNCH_EXACT(8, F8, VM); break;                                                                \
     }
-    if (fast8 && ix.stamps && R == 2 && vmode == 0 && spec) {
+    if (sorted_path) {
+        // pass 1: sorted-array kernel; queries that meet a distance tie go to fb_list
+        if (n > ix.fb_cap) {
+            if (ix.fb_list)
+                DRM_HIP_CHECK(hipFree(ix.fb_list));
+            ix.fb_list = nullptr;
+            DRM_HIP_CHECK(hipMalloc(&ix.fb_list, sizeof(int32_t) * (size_t)n));
+            ix.fb_cap = n;
+        }
+        a.fb_list = ix.fb_list;
+        a.fb_count = ix.counter + 1;
+        if (fast8 && ix.stamps && R == 2)
+            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, true, true>), dim3(slots), dim3(64), lds, stream, a);
+        else if (fast8 && R == 2)
+            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, true>), dim3(slots), dim3(64), lds, stream, a);
+        else if (fast8)
+            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<1, true>), dim3(slots), dim3(64), lds, stream, a);
+        else if (R == 2)
+            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, false>), dim3(slots), dim3(64), lds, stream, a);
+        else
+            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<1, false>), dim3(slots), dim3(64), lds, stream, a);
+        DRM_HIP_CHECK(hipGetLastError());
+        // pass 2: the exact kernel over fb_list (its waves exit at once when the list is empty)
+        a.qlist = ix.fb_list;
+        a.qcount = ix.counter + 1;
+        a.counter = ix.counter + 2;
+        a.stamps = nullptr;
+        if (fast8) { DRM_LAUNCH_EXACT_R(true, 0) } else { DRM_LAUNCH_EXACT_R(false, 0) }
+    } else if (fast8 && ix.stamps && R == 2 && vmode == 0) {
         hipLaunchKernelGGL((hnsw_pq_search_kernel<2, true, 0, true, true>), dim3(slots), dim3(64), lds, stream, a);
     } else if (fast8) {
-        if (vmode == 1) {
-            if (spec) { DRM_LAUNCH_R(true, 1, true) } else { DRM_LAUNCH_R(true, 1, false) }
-        } else {
-            if (spec) { DRM_LAUNCH_R(true, 0, true) } else { DRM_LAUNCH_R(true, 0, false) }
-        }
+        if (vmode == 1) { DRM_LAUNCH_EXACT_R(true, 1) } else { DRM_LAUNCH_EXACT_R(true, 0) }
     } else {
-        if (vmode == 1) { DRM_LAUNCH_R(false, 1, false) } else { DRM_LAUNCH_R(false, 0, false) }
+        if (vmode == 1) { DRM_LAUNCH_EXACT_R(false, 1) } else { DRM_LAUNCH_EXACT_R(false, 0) }
     }
-#undef DRM_LAUNCH_R
-#undef DRM_LAUNCH
+#undef DRM_LAUNCH_EXACT_R
+#undef DRM_LAUNCH_EXACT
     DRM_HIP_CHECK(hipGetLastError());
 }
 

@@ -476,7 +476,7 @@ void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k,
         ix.n_slots = alloc_slots;
     }
     if (!ix.counter)
-        DRM_HIP_CHECK(hipMalloc(&ix.counter, sizeof(uint32_t)));
+        DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
 
     SearchArgs a{};
     a.x = d_x;

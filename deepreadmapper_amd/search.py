@@ -52,6 +52,13 @@ class HnswPqIndex:
                                          d_nhops_upper.ptr if d_nhops_upper is not None else None,
                                          stream.handle if stream is not None else None))
 
+    def fallbacks(self):
+        """Queries of the last search that met a distance tie and took the exact kernel (syncs)."""
+        import ctypes as C
+        c = C.c_int64(0)
+        check(lib().drm_search_fallbacks(self.handle, C.byref(c)))
+        return int(c.value)
+
     def free(self):
         if self._h:
             check(lib().drm_index_free(self._h))

@@ -94,6 +94,9 @@ int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, 
  * contained in nhops (they read M_hnsw-wide rows instead of 2*M_hnsw-wide ones). */
 int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                          int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, void *stream);
+/* Diagnostic (no reference counterpart): how many queries of the last search on this index met an
+ * exact distance tie and were re-run by the exact (faiss heap-layout) kernel. Synchronizes the device. */
+int drm_search_fallbacks(drm_index *index, int64_t *count);
 
 /* ---------------------------------------------------------------- Smith-Waterman rerank */
 /* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):

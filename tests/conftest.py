@@ -46,3 +46,22 @@ def syn20k(tmp_path_factory):
     d = tmp_path_factory.mktemp("syn")
     w = synth.Workload("syn20k", 10_149, 2000, seed=5, read_seed=11).generate(str(d), nthreads=4)
     return {"index": w.index_path, "fx": faiss_file.read(w.index_path), "w": w}
+
+
+@pytest.fixture(scope="session")
+def repeats(tmp_path_factory):
+    """Tie-heavy index: a genome built from a 600 bp unit repeated 6 times inside random flanks, so
+    many windows (and their PQ codes) are identical and equal distances are everywhere. Exercises
+    the exact fallback of the sorted-array search kernel."""
+    from deepreadmapper_amd import synth
+    from oracle import faiss_file
+    d = tmp_path_factory.mktemp("rep")
+    unit = synth.genome(600, seed=3)
+    g = np.concatenate([synth.genome(900, seed=4)] + [unit] * 6 + [synth.genome(900, seed=5)])
+    refs = synth.windows_lookup(g, 150, 1)
+    x = synth.embed(synth.tag(refs))
+    path = str(d / "rep.index")
+    synth.build_index(x, path, nthreads=1)
+    reads, _, _ = synth.simulate_reads(g, 300, seed=13)
+    q = np.concatenate([synth.embed(synth.tag(reads)), x[::29]])  # plus exact window embeddings
+    return {"index": path, "fx": faiss_file.read(path), "x": x, "q": np.ascontiguousarray(q)}

@@ -134,6 +134,25 @@ def test_search_syn20k_bitexact(syn20k):
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
 
 
+@pytest.mark.parametrize("k,ef", [(128, 128), (16, 64), (100, 128)])
+def test_search_ties_fallback(repeats, k, ef):
+    """Repeated genome segments give identical PQ codes: the sorted-array pass must hand those
+    queries to the exact kernel, and the merged output must still equal the oracle bit for bit."""
+    from deepreadmapper_amd import read_index
+    _search_both(repeats["index"], repeats["fx"], repeats["q"], k, ef)
+    ix = read_index(repeats["index"])
+    ix.search(repeats["q"], k, ef)
+    nfb = ix.fallbacks()
+    assert 0 < nfb <= len(repeats["q"])
+
+
+def test_search_exact_kernel_forced(syn20k, monkeypatch):
+    """DRM_SEARCH_EXACT=1 (read at index load) routes every query through the exact kernel."""
+    monkeypatch.setenv("DRM_SEARCH_EXACT", "1")
+    w = syn20k["w"]
+    _search_both(syn20k["index"], syn20k["fx"], w.q_emb[:700], 128, 128)
+
+
 def test_search_device_stats(syn20k):
     from deepreadmapper_amd import read_index
     from deepreadmapper_amd.device import DeviceBuffer, synchronize
