@@ -29,6 +29,7 @@ struct DeviceIndex {
     int32_t has_dup_links = 0; // some neighbour row lists one id twice
     int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
     int32_t force_exact = 0;   // skip the sorted-array pass (every query through the exact kernel)
+    int32_t try_sorted = 0;    // run the sorted-array pass first (DRM_SEARCH_SORTED=1)
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32

@@ -1099,7 +1099,9 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.stamps = ix.stamps;
 
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
-    const bool sorted_path = !ix.force_exact && vmode == 0 && R <= 2;
+    // The sorted-array pass only pays off when distance ties are rare; stride-1 genome windows
+    // share PQ codes so often that nearly every query falls back. Opt-in via DRM_SEARCH_SORTED=1.
+    const bool sorted_path = ix.try_sorted && !ix.force_exact && vmode == 0 && R <= 2;
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 3 * sizeof(uint32_t), stream));
 #define DRM_LAUNCH_EXACT(RR, F8, VM)                                                                           \
     hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, F8>), dim3(slots), dim3(64), lds, stream, a)

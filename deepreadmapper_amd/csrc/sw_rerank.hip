@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "drm_device.h"
 
@@ -25,6 +26,7 @@ namespace drm {
 namespace {
 
 constexpr int kPadRow = 256; // profile row index for "matches nothing"
+constexpr int kNeedBitProfile = -4; // ncand marker: the query needs the bit-profile kernel
 
 // One DP row update for the full register row H[0..LQ).
 template <int LQ>
@@ -194,7 +196,7 @@ __device__ void ps_partial_sort(uint32_t *e, int n, int k)
 
 // Kernel 1 of the rerank: candidate lists (find_sequences static) + one SW score per candidate.
 // One 64-lane workgroup per query (grid-stride); each lane scores two candidates (16-bit halves).
-template <int LQ>
+template <int LQ, bool ONLY_FLAGGED = false>
 __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
 {
     constexpr int NW = (LQ + 15) / 16;
@@ -207,6 +209,8 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
     const int tid = threadIdx.x; // one wave per workgroup
     const int lane = tid & 63;
     for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+        if (ONLY_FLAGGED && a.ncand[q] != kNeedBitProfile)
+            continue; // scored by sw_score_f16_kernel
         const int qlen = a.q_len[q];
         const int nsel = min(a.k_clusters, a.kk);
         const int64_t *nb = a.neighbors + q * a.kk;
@@ -293,6 +297,190 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
             if (has_b) {
                 a.cand_ids[q * a.cmax + c1] = wb;
                 a.cand_scores[q * a.cmax + c1] = (int32_t)best.y;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+
+// ------------------------------------------------------------------------ fp16 DP (fast path)
+// Scores are carried as fp16 multiples of 2^-10 (exact: every value is an integer <= ~300, far
+// below 1024), two candidates per lane. One cell pair is
+//     t = diag + term                     v_pk_add_f16        (term = 2^-9 on a match, else 0)
+//     h = clamp01(max3(t, up, left) - 2^-10)  v_pk_maximum3_f16 + v_pk_add_f16 ... clamp
+// i.e. h = max(0, max3(diag + 2*match, up, left) - 1) scaled by 2^-10; the f16 clamp modifier
+// (to [0, 1]) is the max with 0. The running best takes two columns per v_pk_maximum3_f16.
+// The match term comes from per-class byte profiles: each distinct query byte gets a class
+// (class 0 = matches nothing), cprof[class][j] = 0x18 iff q[j] is that byte, and one v_perm pairs
+// candidate a's and b's bytes of column j into the high bytes of the two halves (0x1800 = 2^-9).
+constexpr int kNcls = 16;             // classes per query (15 distinct bytes + "none")
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+template <int LQ>
+__device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pra, const uint32_t *prb, h2 &best)
+{
+    // the backend forms v_pk_maximum3_f16 from the nested maxima, folds the [0,1] clamp into the
+    // v_pk_add_f16 and merges two columns of `best` into one maximum3
+    const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
+    const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
+    h2 diag = kZero, left = kZero;
+#pragma unroll
+    for (int c16 = 0; c16 < (LQ + 15) / 16; ++c16) {
+        const uint4 A = *reinterpret_cast<const uint4 *>(pra + 4 * c16);
+        const uint4 B = *reinterpret_cast<const uint4 *>(prb + 4 * c16);
+        const uint32_t wa[4] = {A.x, A.y, A.z, A.w};
+        const uint32_t wb[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int j = c16 * 16 + jj;
+            if (j < LQ) {
+                const int w = jj >> 2, bsel = jj & 3;
+                const uint32_t sel = 0x000C000Cu | ((uint32_t)bsel << 8) | ((uint32_t)(4 + bsel) << 24);
+                const h2 term = __builtin_bit_cast(h2, __builtin_amdgcn_perm(wb[w], wa[w], sel));
+                const h2 up = H[j];
+                const h2 t = diag + term;
+                h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(t, up), left);
+                h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
+                diag = up;
+                left = h;
+                H[j] = h;
+                best = __builtin_elementwise_maximum(best, h);
+            }
+        }
+    }
+}
+
+// Kernel 1 (fast path) of the rerank: same contract as sw_score_kernel.
+template <int LQ>
+__global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
+{
+    constexpr int LQP = (LQ + 15) & ~15;
+    __shared__ __align__(16) uint8_t cprof[kNcls * LQP];
+    __shared__ __align__(16) uint8_t cls_map[256];
+    __shared__ __align__(16) uint8_t qbuf[LQP];
+    __shared__ uint64_t cand[kMaxCands];
+    __shared__ int ncand_s, ncls_s;
+
+    const int tid = threadIdx.x; // one wave per workgroup
+    const int lane = tid & 63;
+    for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+        const int qlen = a.q_len[q];
+        const int nsel = min(a.k_clusters, a.kk);
+        const int64_t *nb = a.neighbors + q * a.kk;
+        if (a.stride == 1 && nsel <= kMaxCands) {
+            // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
+            int base = 0;
+            for (int c = 0; c < nsel; c += 64) {
+                const int i = c + lane;
+                const uint64_t id = (i < nsel) ? (uint64_t)nb[i] : ~0ull;
+                const bool keep = id < (uint64_t)a.n_ref;
+                const uint64_t m = __ballot(keep);
+                if (keep)
+                    cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = id;
+                base += __popcll(m);
+            }
+            if (tid == 0)
+                ncand_s = base;
+        } else if (tid == 0) {
+            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride), duplicates kept
+            int nc = 0;
+            bool overflow = false;
+            for (int i = 0; i < nsel && !overflow; ++i) {
+                const uint64_t id = (uint64_t)nb[i];
+                if (a.stride == 1) {
+                    if (id < (uint64_t)a.n_ref) {
+                        if (nc >= kMaxCands)
+                            overflow = true;
+                        else
+                            cand[nc++] = id;
+                    }
+                    continue;
+                }
+                const uint64_t s = (uint64_t)a.stride;
+                const uint64_t actual = id * s;
+                if (actual >= (uint64_t)a.n_ref)
+                    continue;
+                const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
+                const uint64_t end = min(actual + s, (uint64_t)a.n_ref);
+                for (uint64_t pos = start; pos < end; ++pos) {
+                    if (nc >= kMaxCands) {
+                        overflow = true;
+                        break;
+                    }
+                    cand[nc++] = pos;
+                }
+            }
+            ncand_s = overflow ? -2 : nc;
+        }
+        for (int t = tid; t < LQP; t += 64)
+            qbuf[t] = (t < qlen && t < LQ) ? a.queries[q * a.q_stride + t] : 0;
+        reinterpret_cast<uint32_t *>(cls_map)[tid] = 0u;
+        __syncthreads();
+        if (tid == 0) { // classes in first-occurrence order
+            int ncls = 0;
+            for (int j = 0; j < qlen && j < LQ; ++j) {
+                const int b = qbuf[j];
+                if (cls_map[b] == 0) {
+                    if (ncls + 1 >= kNcls) {
+                        ncls = kNcls; // too many distinct bytes: bit-profile kernel
+                        break;
+                    }
+                    cls_map[b] = (uint8_t)(++ncls);
+                }
+            }
+            ncls_s = ncls;
+        }
+        __syncthreads();
+        for (int e = tid; e < kNcls * LQP / 4; e += 64) {
+            const int c = e / (LQP / 4), j0 = (e % (LQP / 4)) * 4;
+            uint32_t word = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                if (c > 0 && j < qlen && j < LQ && cls_map[qbuf[j]] == c)
+                    word |= 0x18u << (8 * u);
+            }
+            reinterpret_cast<uint32_t *>(cprof)[e] = word;
+        }
+        __syncthreads();
+        int ncand = (qlen > LQ) ? -3 : ncand_s;
+        if (ncand >= 0 && ncls_s >= kNcls)
+            ncand = kNeedBitProfile;
+        if (tid == 0)
+            a.ncand[q] = ncand;
+        // two candidates per lane: c and c + 64
+        for (int c0 = tid; c0 < ncand; c0 += 128) {
+            const int c1 = c0 + 64;
+            const bool has_b = c1 < ncand;
+            h2 H[LQ];
+#pragma unroll
+            for (int j = 0; j < LQ; ++j)
+                H[j] = (h2){(_Float16)0.0f, (_Float16)0.0f};
+            h2 best = {(_Float16)0.0f, (_Float16)0.0f};
+            const uint64_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
+            const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
+            const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
+            const int L = a.ref_len;
+            int na = (L > 0) ? (int)pa[0] : -1;
+            int nb2 = (L > 0 && has_b) ? (int)pb[0] : -1;
+            for (int i = 0; i < L; ++i) {
+                const int ca = na, cb = nb2;
+                if (i + 1 < L) { // prefetch the next row's bytes
+                    na = pa[i + 1];
+                    nb2 = has_b ? (int)pb[i + 1] : -1;
+                }
+                const int ka = cls_map[ca];
+                const int kb = cb >= 0 ? (int)cls_map[cb] : 0;
+                sw_row_f16<LQ>(H, reinterpret_cast<const uint32_t *>(cprof + ka * LQP),
+                               reinterpret_cast<const uint32_t *>(cprof + kb * LQP), best);
+            }
+            a.cand_ids[q * a.cmax + c0] = wa;
+            a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);
+            if (has_b) {
+                a.cand_ids[q * a.cmax + c1] = wb;
+                a.cand_scores[q * a.cmax + c1] = (int32_t)((float)best.y * 1024.0f);
             }
         }
         __syncthreads();
@@ -420,15 +608,31 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     a.cand_scores = refs.ws_scores;
     a.ncand = refs.ws_ncand;
     const int grid = (int)std::min<int64_t>(a.nq, 65536);
+    // fp16 class-profile kernel first; the bit-profile kernel then scores only the queries it flagged
+    // (more than kNcls-1 distinct bytes). DRM_SW_BITPROFILE=1 forces the bit-profile kernel.
+    static const bool force_bits = [] {
+        const char *e = std::getenv("DRM_SW_BITPROFILE");
+        return e && std::atoi(e) != 0;
+    }();
     switch (pick_lq(max_qlen)) {
     case 64:
-        hipLaunchKernelGGL(sw_score_kernel<64>, dim3(grid), dim3(64), 0, stream, a);
+        if (force_bits) {
+            hipLaunchKernelGGL((sw_score_kernel<64>), dim3(grid), dim3(64), 0, stream, a);
+        } else {
+            hipLaunchKernelGGL((sw_score_f16_kernel<64>), dim3(grid), dim3(64), 0, stream, a);
+            hipLaunchKernelGGL((sw_score_kernel<64, true>), dim3(grid), dim3(64), 0, stream, a);
+        }
         break;
     case 152:
-        hipLaunchKernelGGL(sw_score_kernel<152>, dim3(grid), dim3(64), 0, stream, a);
+        if (force_bits) {
+            hipLaunchKernelGGL((sw_score_kernel<152>), dim3(grid), dim3(64), 0, stream, a);
+        } else {
+            hipLaunchKernelGGL((sw_score_f16_kernel<152>), dim3(grid), dim3(64), 0, stream, a);
+            hipLaunchKernelGGL((sw_score_kernel<152, true>), dim3(grid), dim3(64), 0, stream, a);
+        }
         break;
     default:
-        hipLaunchKernelGGL(sw_score_kernel<256>, dim3(grid), dim3(64), 0, stream, a);
+        hipLaunchKernelGGL((sw_score_kernel<256>), dim3(grid), dim3(64), 0, stream, a);
         break;
     }
     DRM_HIP_CHECK(hipGetLastError());

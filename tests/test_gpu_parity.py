@@ -68,6 +68,24 @@ def test_rerank_dense_vs_oracle(c1):
     _rerank_both(c1["refs"], I, c1["reads"], 1, 10, 40)  # k < k_clusters
 
 
+def test_rerank_many_distinct_bytes(c1):
+    """Queries over a 40-letter alphabet (more than 15 distinct bytes) take the bit-profile kernel,
+    short/ragged DNA queries the fp16 class-profile kernel; both must equal the oracle, in one batch."""
+    rng = np.random.default_rng(21)
+    refs = rng.integers(33, 73, size=(300, 150)).astype(np.uint8)
+    refs[::3] = c1["refs"][:100]  # some DNA windows too
+    reads = []
+    for i in range(80):
+        if i % 2:
+            reads.append(bytes(rng.integers(33, 73, size=int(rng.integers(1, 153))).astype(np.uint8)))
+        else:
+            r = c1["reads"][i]
+            reads.append(r[: int(rng.integers(1, len(r) + 1))])
+    nb = rng.integers(0, 300, size=(80, 24)).astype(np.int64)
+    _rerank_both(refs, nb, reads, 1, 24, 24)
+    _rerank_both(refs, nb, reads, 1, 5, 20)
+
+
 @pytest.mark.parametrize("stride", [2, 3, 4])
 def test_rerank_sparse_vs_oracle(c1, stride):
     rng = np.random.default_rng(stride)
@@ -134,11 +152,19 @@ def test_search_syn20k_bitexact(syn20k):
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
 
 
+def test_search_syn20k_sorted_pass(syn20k, monkeypatch):
+    """The opt-in sorted-array pass + exact fallback equals the oracle on the dense index."""
+    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
+    w = syn20k["w"]
+    _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
+
+
 @pytest.mark.parametrize("k,ef", [(128, 128), (16, 64), (100, 128)])
-def test_search_ties_fallback(repeats, k, ef):
-    """Repeated genome segments give identical PQ codes: the sorted-array pass must hand those
-    queries to the exact kernel, and the merged output must still equal the oracle bit for bit."""
+def test_search_ties_fallback(repeats, k, ef, monkeypatch):
+    """Repeated genome segments give identical PQ codes: the sorted-array pass (DRM_SEARCH_SORTED=1)
+    must hand those queries to the exact kernel, and the merged output must still equal the oracle."""
     from deepreadmapper_amd import read_index
+    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
     _search_both(repeats["index"], repeats["fx"], repeats["q"], k, ef)
     ix = read_index(repeats["index"])
     ix.search(repeats["q"], k, ef)
@@ -147,7 +173,8 @@ def test_search_ties_fallback(repeats, k, ef):
 
 
 def test_search_exact_kernel_forced(syn20k, monkeypatch):
-    """DRM_SEARCH_EXACT=1 (read at index load) routes every query through the exact kernel."""
+    """DRM_SEARCH_SORTED=1 with DRM_SEARCH_EXACT=1 (read at index load): exact kernel only."""
+    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
     monkeypatch.setenv("DRM_SEARCH_EXACT", "1")
     w = syn20k["w"]
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb[:700], 128, 128)
