@@ -229,8 +229,8 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.force_lds_kernel = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
             if (std::atoi(e)) {
-                DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
-                DRM_HIP_CHECK(hipMemset(d.stamps, 0, 8 * sizeof(uint64_t)));
+                DRM_HIP_CHECK(hipMalloc(&d.stamps, 12 * sizeof(uint64_t)));
+                DRM_HIP_CHECK(hipMemset(d.stamps, 0, 12 * sizeof(uint64_t)));
             }
         try {
             d.centroids = upload_vec(h.centroids, d.device_bytes);
@@ -267,13 +267,13 @@ int drm_index_free(drm_index *index)
 }
 
 // diagnostic (not part of include/drm_hip.h): read and reset the section timers of a stamps build
-int drm_debug_search_stamps(drm_index *index, uint64_t *out8)
+int drm_debug_search_stamps(drm_index *index, uint64_t *out12)
 {
     return guarded([&] {
         if (!index || !index->dev.stamps)
             throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
-        DRM_HIP_CHECK(hipMemcpy(out8, index->dev.stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 8 * sizeof(uint64_t)));
+        DRM_HIP_CHECK(hipMemcpy(out12, index->dev.stamps, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 12 * sizeof(uint64_t)));
     });
 }
 

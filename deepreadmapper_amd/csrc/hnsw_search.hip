@@ -267,6 +267,154 @@ template <int R> __device__ void heap_pop_par(uint32_t (&hk)[R], uint32_t (&hi)[
     }
 }
 
+
+// Candidate heap (faiss MinimaxHeap arrays; 1-based heap index i = slot + 1) for ef <= 128 in the
+// sibling-pair layout: lane p holds the two children of node slot p, slots 2p+1 (L) and 2p+2 (R).
+// Slot 0, the root, sits in lane 63's R half (node 63's right child would be slot 128 >= ef).
+// A sift-down then picks every node's larger child inside its own lane, the path values are one
+// ds_bpermute of the chosen children, and each pair's new contents come from one source lane.
+struct PairHeap {
+    uint32_t kL, kR, iL, iR;
+
+    __device__ __forceinline__ void init()
+    {
+        kL = kR = 0u;
+        iL = iR = 0xFFFFFFFFu;
+    }
+    static __device__ __forceinline__ int lane_of(int s) { return s == 0 ? 63 : (s - 1) >> 1; }
+    static __device__ __forceinline__ bool right_of(int s) { return s == 0 || ((s - 1) & 1); }
+    // (values are selected, never members: a member chosen at run time would be spilled to scratch)
+    __device__ __forceinline__ uint32_t key(int s) const
+    {
+        const int l = lane_of(s);
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)kL, l);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)kR, l);
+        return right_of(s) ? b : a;
+    }
+    __device__ __forceinline__ uint32_t id(int s) const
+    {
+        const int l = lane_of(s);
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)iL, l);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)iR, l);
+        return right_of(s) ? b : a;
+    }
+    __device__ __forceinline__ void set(int s, uint32_t k, uint32_t i)
+    {
+        const bool mine = lane_id() == lane_of(s);
+        const bool r = right_of(s);
+        const bool mr = mine && r, ml = mine && !r;
+        kR = mr ? k : kR;
+        iR = mr ? i : iR;
+        kL = ml ? k : kL;
+        iL = ml ? i : iL;
+    }
+    __device__ __forceinline__ void set_id(int s, uint32_t i)
+    {
+        const bool mine = lane_id() == lane_of(s);
+        const bool r = right_of(s);
+        iR = (mine && r) ? i : iR;
+        iL = (mine && !r) ? i : iL;
+    }
+    __device__ __forceinline__ uint32_t root_key() const { return (uint32_t)__builtin_amdgcn_readlane((int)kR, 63); }
+    __device__ __forceinline__ uint32_t root_id() const { return (uint32_t)__builtin_amdgcn_readlane((int)iR, 63); }
+
+    // faiss heap_push<CMax<float,int32>>(k, key, id): the new element starts at 1-based index k
+    __device__ __forceinline__ void push(int k, uint32_t key_, int32_t id_)
+    {
+        if (k == 1 || !cmp2(key_, key((k >> 1) - 1), id_, (int32_t)id((k >> 1) - 1))) {
+            set(k - 1, key_, (uint32_t)id_); // most pushes stay at the bottom
+            return;
+        }
+        const int lane = lane_id();
+        // lane l >= 1: the ancestor k >> l; the sift-up passes every ancestor below the new element
+        const int anc = (lane < 16) ? (k >> lane) : 0;
+        const bool exists = lane >= 1 && anc >= 1;
+        const int sa = exists ? anc - 1 : 0;
+        const int sl = lane_of(sa);
+        const bool sr = right_of(sa);
+        const uint32_t akL = (uint32_t)__shfl((int)kL, sl, 64), akR = (uint32_t)__shfl((int)kR, sl, 64);
+        const uint32_t aiL = (uint32_t)__shfl((int)iL, sl, 64), aiR = (uint32_t)__shfl((int)iR, sl, 64);
+        const uint32_t ak = sr ? akR : akL, ai = sr ? aiR : aiL;
+        const bool moves = exists && cmp2(key_, ak, id_, (int32_t)ai);
+        const int h = __builtin_ctzll(__ballot(lane >= 1 && !moves)) - 1; // ancestors 1..h move down
+        const int bk = 32 - __builtin_clz((unsigned)k);
+        // chain index m holds the node k >> m; it receives chain m+1's value, chain h the new one
+        {
+            const int m = bk - 1; // the root
+            if (m <= h) {
+                const uint32_t nk = (m == h) ? key_ : (uint32_t)__builtin_amdgcn_readlane((int)ak, m + 1);
+                const uint32_t ni = (m == h) ? (uint32_t)id_ : (uint32_t)__builtin_amdgcn_readlane((int)ai, m + 1);
+                kR = (lane == 63) ? nk : kR;
+                iR = (lane == 63) ? ni : iR;
+            }
+        }
+        const int iLx = 2 * lane + 2; // 1-based index of this lane's L slot (R = iLx + 1)
+        const int m = bk - (32 - __builtin_clz((unsigned)iLx));
+        const bool inrange = m >= 0 && m <= h;
+        const int tgt = inrange ? (k >> m) : 0;
+        const bool onL = inrange && tgt == iLx;
+        const bool onR = inrange && tgt == iLx + 1 && lane != 63;
+        const int src = (m + 1) & 63;
+        const uint32_t vk = (uint32_t)__shfl((int)ak, src, 64), vi = (uint32_t)__shfl((int)ai, src, 64);
+        const uint32_t nk = (m == h) ? key_ : vk, ni = (m == h) ? (uint32_t)id_ : vi;
+        if (onL) {
+            kL = nk;
+            iL = ni;
+        }
+        if (onR) {
+            kR = nk;
+            iR = ni;
+        }
+    }
+
+    // faiss heap_pop<CMax<float,int32>>(k): the element at 1-based k is sifted down from the root
+    __device__ __forceinline__ void pop(int k)
+    {
+        const int lane = lane_id();
+        const uint32_t vk = key(k - 1);
+        const int32_t vi = (int32_t)id(k - 1);
+        // node `lane` (1-based lane+1) has children 2*lane+2 (L) and 2*lane+3 (R); node 63's only
+        // possible child is 128
+        const bool takeL = (lane == 63) || (2 * lane + 3 == k + 1) || cmp2(kL, kR, (int32_t)iL, (int32_t)iR);
+        const uint64_t lm = __ballot(takeL);
+        const uint32_t mk = takeL ? kL : kR, mi = takeL ? iL : iR;
+        int leaf = 1, depth = 0;
+        while (2 * leaf <= k) {
+            leaf = 2 * leaf + (int)(((lm >> (leaf - 1)) & 1ull) ^ 1ull);
+            ++depth;
+        }
+        // lane l in [1, depth]: the path node at depth l = the chosen child of the node above it
+        const bool onpath = lane >= 1 && lane <= depth;
+        const int par = onpath ? (leaf >> (depth - lane + 1)) - 1 : 0;
+        const uint32_t ak = (uint32_t)__shfl((int)mk, par, 64), ai = (uint32_t)__shfl((int)mi, par, 64);
+        const int h = __builtin_ctzll(__ballot(lane >= 1 && (!onpath || cmp2(vk, ak, vi, (int32_t)ai)))) - 1;
+        // depth m takes depth m+1's value for m < h; depth h takes the sifted element
+        {
+            const uint32_t nk = (h == 0) ? vk : (uint32_t)__builtin_amdgcn_readlane((int)ak, 1);
+            const uint32_t ni = (h == 0) ? (uint32_t)vi : (uint32_t)__builtin_amdgcn_readlane((int)ai, 1);
+            kR = (lane == 63) ? nk : kR;
+            iR = (lane == 63) ? ni : iR;
+        }
+        const int iLx = 2 * lane + 2;
+        const int m = 31 - __builtin_clz((unsigned)iLx); // depth of this lane's pair
+        const bool inrange = m <= h;
+        const int tgt = inrange ? (leaf >> (depth - m)) : 0;
+        const bool onL = inrange && tgt == iLx;
+        const bool onR = inrange && tgt == iLx + 1 && lane != 63;
+        const int src = (m + 1) & 63;
+        const uint32_t wk = (uint32_t)__shfl((int)ak, src, 64), wi = (uint32_t)__shfl((int)ai, src, 64);
+        const uint32_t nk = (m == h) ? vk : wk, ni = (m == h) ? (uint32_t)vi : wi;
+        if (onL) {
+            kL = nk;
+            iL = ni;
+        }
+        if (onR) {
+            kR = nk;
+            iR = ni;
+        }
+    }
+};
+
 // PQ ADC distance of node v: sequential fp32 sum over sub-quantizers starting from 0
 // (distance_single_code / distance_four_codes for M < 16) [upstream faiss].
 template <bool FAST8>
@@ -435,7 +583,7 @@ template <int R, bool FAST8, int VMODE, bool SPEC, bool STAMPS = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hnsw_pq_search_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
@@ -487,11 +635,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
 
         DRM_STAMP(1);
         // --- level 0. Result handler: k slots of (+inf,-1) (HeapBlockResultHandler::begin)
-        uint32_t rk[R], ri[R], ck[R], ci[R];
+        constexpr bool PAIR = R <= 2; // candidate heap in the sibling-pair layout (ef <= 128)
+        uint32_t rk[R], ri[R], ck[PAIR ? 1 : R], ci[PAIR ? 1 : R];
+        PairHeap ph;
+        ph.init();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             rk[r] = kInfKey;
             ri[r] = 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int r = 0; r < (PAIR ? 1 : R); ++r) {
             ck[r] = 0;
             ci[r] = 0xFFFFFFFFu;
         }
@@ -527,8 +681,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         };
         // MinimaxHeap candidates(ef); push(nearest, d_nearest); seed result + visited set
         int kc = 1, nvalid = 1;
-        wr(ck, 0, dn);
-        wr(ci, 0, (uint32_t)nearest);
+        if constexpr (PAIR) {
+            ph.set(0, dn, (uint32_t)nearest);
+        } else {
+            wr(ck, 0, dn);
+            wr(ci, 0, (uint32_t)nearest);
+        }
         add_result(dn, nearest);
         int clear_n = 0, hcount = 0;
         bool spilled = (VMODE == 0);
@@ -551,29 +709,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         while (nvalid > 0) {
             // pop_min: smallest distance among valid slots, ties -> highest slot
             uint32_t bh = 0xFFFFFFFFu, bl = 0xFFFFFFFFu;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int s = lane + 64 * r;
-                if (s < kc && ci[r] != 0xFFFFFFFFu) {
-                    const uint32_t lo = 0xFFFFFFFFu - (uint32_t)s;
-                    if (ck[r] < bh || (ck[r] == bh && lo < bl)) {
-                        bh = ck[r];
+            const int sL = 2 * lane + 1, sR = (lane == 63) ? 0 : 2 * lane + 2; // PAIR slots of this lane
+            if constexpr (PAIR) {
+                if (sR < kc && ph.iR != 0xFFFFFFFFu) {
+                    bh = ph.kR;
+                    bl = 0xFFFFFFFFu - (uint32_t)sR;
+                }
+                if (sL < kc && ph.iL != 0xFFFFFFFFu) {
+                    const uint32_t lo = 0xFFFFFFFFu - (uint32_t)sL;
+                    if (ph.kL < bh || (ph.kL == bh && lo < bl)) {
+                        bh = ph.kL;
                         bl = lo;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int s = lane + 64 * r;
+                    if (s < kc && ci[r] != 0xFFFFFFFFu) {
+                        const uint32_t lo = 0xFFFFFFFFu - (uint32_t)s;
+                        if (ck[r] < bh || (ck[r] == bh && lo < bl)) {
+                            bh = ck[r];
+                            bl = lo;
+                        }
                     }
                 }
             }
             const uint64_t best = wave_min_pair(bh, bl);
             const int imin = (int)ufirst(0xFFFFFFFFu - (uint32_t)best);
             const uint32_t d0 = ufirst((uint32_t)(best >> 32));
-            const int32_t v0 = (int32_t)rd(ci, imin);
-            wr(ci, imin, 0xFFFFFFFFu);
+            int32_t v0;
+            if constexpr (PAIR) {
+                v0 = (int32_t)ph.id(imin);
+                ph.set_id(imin, 0xFFFFFFFFu);
+            } else {
+                v0 = (int32_t)rd(ci, imin);
+                wr(ci, imin, 0xFFFFFFFFu);
+            }
             nvalid--;
             // count_below(d0): every slot < kc, popped ones included
             int below = 0;
+            if constexpr (PAIR) {
+                below = __popcll(__ballot(sL < kc && ph.kL < d0)) + __popcll(__ballot(sR < kc && ph.kR < d0));
+            } else {
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int s = lane + 64 * r;
-                below += __popcll(__ballot(s < kc && ck[r] < d0));
+                for (int r = 0; r < R; ++r) {
+                    const int s = lane + 64 * r;
+                    below += __popcll(__ballot(s < kc && ck[r] < d0));
+                }
             }
             if (below >= a.efSearch)
                 break;
@@ -653,12 +836,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
                 // prediction (ties, evictions) only costs a reload.
                 uint32_t mk = fresh ? dk : 0xFFFFFFFFu;
                 uint32_t mid = (uint32_t)v1;
+                if constexpr (PAIR) {
+                    const int sL = 2 * lane + 1, sR = (lane == 63) ? 0 : 2 * lane + 2;
+                    if (sL < kc && ph.iL != 0xFFFFFFFFu && ph.kL < mk) {
+                        mk = ph.kL;
+                        mid = ph.iL;
+                    }
+                    if (sR < kc && ph.iR != 0xFFFFFFFFu && ph.kR < mk) {
+                        mk = ph.kR;
+                        mid = ph.iR;
+                    }
+                } else {
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int s = lane + 64 * r;
-                    if (s < kc && ci[r] != 0xFFFFFFFFu && ck[r] < mk) {
-                        mk = ck[r];
-                        mid = ci[r];
+                    for (int r = 0; r < R; ++r) {
+                        const int s = lane + 64 * r;
+                        if (s < kc && ci[r] != 0xFFFFFFFFu && ck[r] < mk) {
+                            mk = ck[r];
+                            mid = ci[r];
+                        }
                     }
                 }
                 const uint32_t m = wave_min_u32(mk);
@@ -682,36 +877,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
                 rem &= rem - 1;
                 const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
                 const int32_t id = __builtin_amdgcn_readlane(v1, l);
+                DRM_STAMP(5);
                 add_result(key, id);
+                DRM_STAMP(8);
                 if (kc == a.ef) { // MinimaxHeap::push on a full heap
-                    if (key >= (uint32_t)__builtin_amdgcn_readlane((int)ck[0], 0))
-                        continue;
-                    if ((uint32_t)__builtin_amdgcn_readlane((int)ci[0], 0) != 0xFFFFFFFFu)
-                        --nvalid;
-                    if (R <= 2)
-                        heap_pop_par(ck, ci, kc);
-                    else
+                    if constexpr (PAIR) {
+                        if (key >= ph.root_key())
+                            continue;
+                        if (ph.root_id() != 0xFFFFFFFFu)
+                            --nvalid;
+                        ph.pop(kc);
+                        DRM_STAMP(9);
+                    } else {
+                        if (key >= (uint32_t)__builtin_amdgcn_readlane((int)ck[0], 0))
+                            continue;
+                        if ((uint32_t)__builtin_amdgcn_readlane((int)ci[0], 0) != 0xFFFFFFFFu)
+                            --nvalid;
                         heap_pop(ck, ci, kc);
+                    }
                     kc--;
                 }
                 kc++;
-                if (R <= 2) {
-                    // most pushes stay at the bottom: test the parent with one uniform read first
-                    bool moves = false;
-                    if (kc > 1) {
-                        const int par = (kc >> 1) - 1;
-                        moves = cmp2(key, rd(ck, par), id, (int32_t)rd(ci, par));
-                    }
-                    if (moves) {
-                        heap_push_par(ck, ci, kc, key, id);
-                    } else {
-                        wr(ck, kc - 1, key);
-                        wr(ci, kc - 1, (uint32_t)id);
-                    }
-                } else {
+                if constexpr (PAIR)
+                    ph.push(kc, key, id);
+                else
                     heap_push(ck, ci, kc, key, id);
-                }
                 ++nvalid;
+                DRM_STAMP(10);
             }
             nstep++;
             DRM_STAMP(5);
@@ -751,7 +943,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         DRM_STAMP(6);
     }
     if (STAMPS && lane_id() == 0 && a.stamps)
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
@@ -772,7 +964,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
@@ -999,7 +1191,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         DRM_STAMP(6);
     }
     if (STAMPS && lane_id() == 0 && a.stamps)
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 

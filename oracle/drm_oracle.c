@@ -230,9 +230,9 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
  * ====================================================================================== */
 
 /* operation counters (diagnostic; summed over all queries of the last oracle_hnswpq_search call) */
-static int64_t g_cnt_push, g_cnt_pop, g_cnt_reject, g_cnt_result;
+static int64_t g_cnt_push, g_cnt_pop, g_cnt_reject, g_cnt_result, g_cnt_tiepop, g_cnt_tieq;
 /* per-thread tallies, folded into the globals once per thread (no atomics in the hot loop) */
-static _Thread_local int64_t t_push, t_pop, t_reject, t_result;
+static _Thread_local int64_t t_push, t_pop, t_reject, t_result, t_tiepop, t_tieq;
 /* faiss::CMax<T,TI>::cmp2 -- (a1 > b1) || (a1 == b1 && a2 > b2) */
 #define CMP2(v1, v2, i1, i2) (((v1) > (v2)) || (((v1) == (v2)) && ((i1) > (i2))))
 
@@ -414,6 +414,11 @@ static int32_t mm_pop_min(minimax_t *h, float *vmin_out)
     }
     if (vmin_out)
         *vmin_out = vmin;
+    for (int j = 0; j < h->k; ++j) /* diagnostic: another valid slot holds the same minimum */
+        if (j != imin && h->ids[j] != -1 && h->dis[j] == vmin) {
+            t_tiepop++;
+            break;
+        }
     int32_t ret = h->ids[imin];
     h->ids[imin] = -1;
     --h->nvalid;
@@ -473,12 +478,14 @@ static inline float pq_dis(const oracle_hnswpq_t *ix, const float *lut, int64_t 
     return r;
 }
 
-void oracle_hnsw_counters(int64_t *out4)
+void oracle_hnsw_counters(int64_t *out6)
 {
-    out4[0] = g_cnt_push;
-    out4[1] = g_cnt_pop;
-    out4[2] = g_cnt_reject;
-    out4[3] = g_cnt_result;
+    out6[0] = g_cnt_push;
+    out6[1] = g_cnt_pop;
+    out6[2] = g_cnt_reject;
+    out6[3] = g_cnt_result;
+    out6[4] = g_cnt_tiepop;
+    out6[5] = g_cnt_tieq;
 }
 
 typedef struct {
@@ -604,7 +611,7 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
 {
     if (k <= 0)
         return -1;
-    g_cnt_push = g_cnt_pop = g_cnt_reject = g_cnt_result = 0;
+    g_cnt_push = g_cnt_pop = g_cnt_reject = g_cnt_result = g_cnt_tiepop = g_cnt_tieq = 0;
     const int ef = efSearch > k ? efSearch : k;
 #ifdef _OPENMP
     if (nthreads <= 0)
@@ -618,12 +625,15 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
         s.visno = 1;
         s.cand.ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)ef);
         s.cand.dis = (float *)malloc(sizeof(float) * (size_t)ef);
-        t_push = t_pop = t_reject = t_result = 0;
+        t_push = t_pop = t_reject = t_result = t_tiepop = t_tieq = 0;
 #ifdef _OPENMP
 #pragma omp for schedule(guided)
 #endif
-        for (int64_t i = 0; i < n; ++i)
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t tp0 = t_tiepop;
             hnsw_search_one(ix, x + i * ix->d, k, efSearch, D + i * k, I + i * k, ndis + i, nhops + i, &s);
+            t_tieq += t_tiepop != tp0;
+        }
 #ifdef _OPENMP
 #pragma omp critical
 #endif
@@ -632,6 +642,8 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
             g_cnt_pop += t_pop;
             g_cnt_reject += t_reject;
             g_cnt_result += t_result;
+            g_cnt_tiepop += t_tiepop;
+            g_cnt_tieq += t_tieq;
         }
         free(s.lut);
         free(s.visited);

@@ -67,7 +67,9 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
                          float *D, int64_t *I, int32_t *ndis, int32_t *nhops, int nthreads);
 
 /* diagnostic: {candidate pushes, pops on full heap, rejected pushes, result insertions} of the last search */
-void oracle_hnsw_counters(int64_t *out4);
+/* diagnostic op counts of the last oracle_hnswpq_search: push, pop(evict), reject, result insert,
+ * pop_min calls facing an equal valid minimum, queries with at least one such pop_min */
+void oracle_hnsw_counters(int64_t *out6);
 
 #ifdef __cplusplus
 }

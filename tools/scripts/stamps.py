@@ -19,12 +19,13 @@ dq = DeviceBuffer.from_host(w.q_emb[:Q])
 dD, dI = DeviceBuffer((Q, 128), np.float32), DeviceBuffer((Q, 128), np.int64)
 ix.search_device(dq, Q, 128, 128, dD, dI)
 synchronize()
-out = np.zeros(8, dtype=np.uint64)
+out = np.zeros(12, dtype=np.uint64)
 L = lib()
 L.drm_debug_search_stamps.argtypes = [C.c_void_p, C.c_void_p]
 check(L.drm_debug_search_stamps(ix.handle, out.ctypes.data))
-names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances(LUT sum)",
-         "add_to_heap loop", "output+clear", "queue/top"]
+names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances+prefetch",
+         "push loop: fetch/reject/overhead", "output+clear", "queue/top", "push loop: add_result",
+         "push loop: evict (heap_pop)", "push loop: heap_push", "-"]
 tot = float(out.sum())
 for n, v in zip(names, out):
     print(f"{n:28s} {v / tot * 100:6.2f} %")
