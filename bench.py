@@ -25,6 +25,35 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
+SEARCH_KERNEL = "hnsw_pq_search_kernel<2, true, 0, true, false>"  # what C3 (ef = k = 128, PQ8x8) launches
+SW_KERNEL = "sw_score_f16_kernel<152>"
+SW_VALU_PER_CELL = 684 / 152 / 2  # static ISA count of sw_row_f16<152>: 684 VALU per row of 152 cell pairs
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def committed_pmc(kernel_substr):
+    """Per-dispatch PMC summary of `kernel_substr` from the newest committed profile
+    (profiles/rNN/summary.json, written by tools/scripts/profile.sh + summarize_profile.py)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")), reverse=True):
+        try:
+            ks = json.load(open(path))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, v in ks.items():
+            if kernel_substr in name:
+                return os.path.relpath(path, ROOT), v
+    return None, None
 
 
 def log(*a):
@@ -88,8 +117,8 @@ def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn):
     ts, tw = run(n)
     log_fn(f"[cpu] oracle on {n} queries x {threads} threads: search {ts:.2f}s, SW {tw:.2f}s")
     return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of this rank's C3 reads (oracle/ C restatement, OpenMP {threads} threads): "
-                      f"search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+            "sample": f"first {n} of this rank's C3 reads (oracle/ C restatement, OpenMP {threads} threads on "
+                      f"{cpu_model()}): search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
 
 
 def main():
@@ -193,6 +222,15 @@ def main():
     bytes_launch = float(bytes_q.sum() + codebook)
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
     cells = float(Q) * K * w.refs.shape[1] * queries.shape[1]
+    prof_path, pmc = committed_pmc(SEARCH_KERNEL)
+    traffic = None
+    if pmc and "hbm_bytes_est" in pmc:
+        traffic = float(pmc["hbm_bytes_est"])
+    sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL)
+    ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
+    sw_gcups = cells / (sw_ms * 1e-3) / 1e9
+    # VALU issue ceiling of the SW DP: 4 SIMD x 16 lanes per CU, 2 cells per packed lane-op
+    sw_peak_gcups = ncu * 64 * CLOCK_HZ / SW_VALU_PER_CELL / 1e9
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
@@ -211,10 +249,21 @@ def main():
                                    "EFC=200), search + SW rerank, EF=128 K=128",
                        "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
-            "roofline": {"bound": "hbm", "kernel": "hnsw_pq_search_kernel", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": SEARCH_KERNEL, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": round(search_ms, 4)},
+                         "traffic": traffic, "bytes_per_launch": bytes_launch,
+                         "avg_launch_ms": round(search_ms, 4),
+                         "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch, gfx950 x2 "
+                                            "read correction, uncalibrated for 4-8 B random reads")
+                         if traffic is not None else None,
+                         "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
+                         if pmc and "valu_issue_frac" in pmc else None},
+            "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_gcups, 1),
+                            "peak": round(sw_peak_gcups, 1), "unit": "GCUPS",
+                            "frac": round(sw_gcups / sw_peak_gcups, 4),
+                            "valu_ops_per_cell": SW_VALU_PER_CELL,
+                            "valu_issue_frac_pmc": round(sw_pmc["valu_issue_frac"], 3)
+                            if sw_pmc and "valu_issue_frac" in sw_pmc else None},
             "cpu_baseline": cpu,
             "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),

@@ -17,3 +17,4 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU S
   timeout -k 10 600 rocprofv3 --pmc $set -d $OUT/pmc$i -o run --output-format csv -- $BENCH > $OUT/pmc${i}_bench.json 2> $OUT/pmc${i}.err || { echo "pmc pass $i failed ($set)"; tail -3 $OUT/pmc${i}.err; }
 done
 find $OUT -name "*.csv" | head -20
+python3 tools/scripts/summarize_profile.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
