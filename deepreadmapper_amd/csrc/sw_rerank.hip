@@ -321,34 +321,39 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 template <int LQ>
 __device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pra, const uint32_t *prb, h2 &best)
 {
-    // the backend forms v_pk_maximum3_f16 from the nested maxima, folds the [0,1] clamp into the
-    // v_pk_add_f16 and merges two columns of `best` into one maximum3
+    // The backend forms v_pk_maximum3_f16 from the nested maxima, folds the [0,1] clamp into the
+    // v_pk_add_f16 and merges two columns of `best` into one maximum3. The next column's diagonal
+    // term (old H[j] + term) is formed before H[j] is overwritten, so H stays in place (no v_mov).
     const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
     const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
-    h2 diag = kZero, left = kZero;
+    constexpr int NC16 = (LQ + 15) / 16;
+    uint32_t wa[NC16][4], wb[NC16][4];
 #pragma unroll
-    for (int c16 = 0; c16 < (LQ + 15) / 16; ++c16) {
+    for (int c16 = 0; c16 < NC16; ++c16) {
         const uint4 A = *reinterpret_cast<const uint4 *>(pra + 4 * c16);
         const uint4 B = *reinterpret_cast<const uint4 *>(prb + 4 * c16);
-        const uint32_t wa[4] = {A.x, A.y, A.z, A.w};
-        const uint32_t wb[4] = {B.x, B.y, B.z, B.w};
+        wa[c16][0] = A.x, wa[c16][1] = A.y, wa[c16][2] = A.z, wa[c16][3] = A.w;
+        wb[c16][0] = B.x, wb[c16][1] = B.y, wb[c16][2] = B.z, wb[c16][3] = B.w;
+    }
+    auto term = [&](int j) {
+        const int c16 = j >> 4, w = (j >> 2) & 3, bsel = j & 3;
+        const uint32_t sel = 0x000C000Cu | ((uint32_t)bsel << 8) | ((uint32_t)(4 + bsel) << 24);
+        return __builtin_bit_cast(h2, __builtin_amdgcn_perm(wb[c16][w], wa[c16][w], sel));
+    };
+    h2 t = term(0); // diag of column 0 is the zero border
+    h2 left = kZero;
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            const int j = c16 * 16 + jj;
-            if (j < LQ) {
-                const int w = jj >> 2, bsel = jj & 3;
-                const uint32_t sel = 0x000C000Cu | ((uint32_t)bsel << 8) | ((uint32_t)(4 + bsel) << 24);
-                const h2 term = __builtin_bit_cast(h2, __builtin_amdgcn_perm(wb[w], wa[w], sel));
-                const h2 up = H[j];
-                const h2 t = diag + term;
-                h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(t, up), left);
-                h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
-                diag = up;
-                left = h;
-                H[j] = h;
-                best = __builtin_elementwise_maximum(best, h);
-            }
-        }
+    for (int j = 0; j < LQ; ++j) {
+        const h2 up = H[j];
+        h2 tn = kZero;
+        if (j + 1 < LQ)
+            tn = up + term(j + 1);
+        h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(t, up), left);
+        h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
+        H[j] = h;
+        left = h;
+        best = __builtin_elementwise_maximum(best, h);
+        t = tn;
     }
 }
 
