@@ -26,7 +26,6 @@ namespace drm {
 namespace {
 
 constexpr int kPadRow = 256; // profile row index for "matches nothing"
-constexpr int kNeedBitProfile = -4; // ncand marker: the query needs the bit-profile kernel
 
 // One DP row update for the full register row H[0..LQ).
 template <int LQ>
@@ -209,7 +208,7 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
     const int tid = threadIdx.x; // one wave per workgroup
     const int lane = tid & 63;
     for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
-        if (ONLY_FLAGGED && a.ncand[q] != kNeedBitProfile)
+        if (ONLY_FLAGGED && a.ncand[q] != -4)
             continue; // scored by sw_score_f16_kernel
         const int qlen = a.q_len[q];
         const int nsel = min(a.k_clusters, a.kk);
@@ -306,67 +305,69 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
 
 // ------------------------------------------------------------------------ fp16 DP (fast path)
 // Scores are carried as fp16 multiples of 2^-10 (exact: every value is an integer <= ~300, far
-// below 1024), two candidates per lane. One cell pair is
-//     t = diag + term                     v_pk_add_f16        (term = 2^-9 on a match, else 0)
-//     h = clamp01(max3(t, up, left) - 2^-10)  v_pk_maximum3_f16 + v_pk_add_f16 ... clamp
-// i.e. h = max(0, max3(diag + 2*match, up, left) - 1) scaled by 2^-10; the f16 clamp modifier
-// (to [0, 1]) is the max with 0. The running best takes two columns per v_pk_maximum3_f16.
-// The match term comes from per-class byte profiles: each distinct query byte gets a class
-// (class 0 = matches nothing), cprof[class][j] = 0x18 iff q[j] is that byte, and one v_perm pairs
-// candidate a's and b's bytes of column j into the high bytes of the two halves (0x1800 = 2^-9).
-constexpr int kNcls = 16;             // classes per query (15 distinct bytes + "none")
-
+// below 1024), two candidates per lane in the halves of one register. One cell pair is
+//     t = diag + term                         v_pk_add_f16   (term = 2^-9 on a match, else 0)
+//     h = clamp01(max3(t, up, left) - 2^-10)  v_pk_maximum3_f16, v_pk_add_f16 ... clamp
+// i.e. h = max(0, max3(diag + 2*match, up, left) - 1) scaled by 2^-10 (metrics.cpp:34-37); the
+// f16 clamp modifier (to [0, 1]) is the max with 0, and the running best takes two columns per
+// v_pk_maximum3_f16 -- 3.5 VALU per cell pair.
+//
+// The match terms come ready-paired from LDS: for candidate-byte codes a, b in 0..4 (A, C, G, T,
+// 4 = "a byte the query does not contain") `pprof` row (a, b) holds the words
+// (q[j]==a ? 0x1800 : 0) | (q[j]==b ? 0x18000000 : 0) (0x1800 = 2^-9 in fp16). A candidate byte that
+// is not A/C/G/T but does occur in the query (e.g. N against N) cannot be coded; the query is then
+// flagged (ncand = kNeedBitProfile) and the bit-profile kernel re-scores it exactly.
+constexpr int kNeedBitProfile = -4;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
-template <int LQ>
-__device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pra, const uint32_t *prb, h2 &best)
+__device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
 {
-    // The backend forms v_pk_maximum3_f16 from the nested maxima, folds the [0,1] clamp into the
-    // v_pk_add_f16 and merges two columns of `best` into one maximum3. The next column's diagonal
-    // term (old H[j] + term) is formed before H[j] is overwritten, so H stays in place (no v_mov).
+    const int k = (c >> 1) & 3; // A=0x41 -> 0, C=0x43 -> 1, T=0x54 -> 2, G=0x47 -> 3
+    return (((0x47544341u >> (8 * k)) & 0xFFu) == (uint32_t)c) ? k : -1;
+}
+__device__ __forceinline__ int acgt_byte(int k) { return k < 4 ? (int)((0x47544341u >> (8 * k)) & 0xFFu) : -1; }
+
+template <int LQ>
+__device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pp, h2 &best)
+{
     const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
     const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
-    constexpr int NC16 = (LQ + 15) / 16;
-    uint32_t wa[NC16][4], wb[NC16][4];
-#pragma unroll
-    for (int c16 = 0; c16 < NC16; ++c16) {
-        const uint4 A = *reinterpret_cast<const uint4 *>(pra + 4 * c16);
-        const uint4 B = *reinterpret_cast<const uint4 *>(prb + 4 * c16);
-        wa[c16][0] = A.x, wa[c16][1] = A.y, wa[c16][2] = A.z, wa[c16][3] = A.w;
-        wb[c16][0] = B.x, wb[c16][1] = B.y, wb[c16][2] = B.z, wb[c16][3] = B.w;
-    }
-    auto term = [&](int j) {
-        const int c16 = j >> 4, w = (j >> 2) & 3, bsel = j & 3;
-        const uint32_t sel = 0x000C000Cu | ((uint32_t)bsel << 8) | ((uint32_t)(4 + bsel) << 24);
-        return __builtin_bit_cast(h2, __builtin_amdgcn_perm(wb[c16][w], wa[c16][w], sel));
-    };
-    h2 t = term(0); // diag of column 0 is the zero border
+    uint4 P = *reinterpret_cast<const uint4 *>(pp);
+    h2 td = __builtin_bit_cast(h2, P.x); // column 0: the diagonal is the zero border
     h2 left = kZero;
 #pragma unroll
     for (int j = 0; j < LQ; ++j) {
         const h2 up = H[j];
+        // the next column's diag + term is formed from old H[j] before H[j] is overwritten, so H
+        // stays in place across rows (no register rotation)
         h2 tn = kZero;
-        if (j + 1 < LQ)
-            tn = up + term(j + 1);
-        h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(t, up), left);
+        if (j + 1 < LQ) {
+            const int n = j + 1;
+            if ((n & 3) == 0)
+                P = *reinterpret_cast<const uint4 *>(pp + n);
+            const uint32_t w = (n & 3) == 0 ? P.x : (n & 3) == 1 ? P.y : (n & 3) == 2 ? P.z : P.w;
+            tn = up + __builtin_bit_cast(h2, w);
+        }
+        h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(td, up), left);
         h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
         H[j] = h;
         left = h;
         best = __builtin_elementwise_maximum(best, h);
-        t = tn;
+        td = tn;
     }
 }
 
-// Kernel 1 (fast path) of the rerank: same contract as sw_score_kernel.
+// Kernel 1 (fast path) of the rerank: candidate lists (find_sequences static) + one SW score per
+// candidate; same contract as sw_score_kernel. One 64-lane workgroup per query (grid-stride).
 template <int LQ>
 __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
 {
-    constexpr int LQP = (LQ + 15) & ~15;
-    __shared__ __align__(16) uint8_t cprof[kNcls * LQP];
-    __shared__ __align__(16) uint8_t cls_map[256];
-    __shared__ __align__(16) uint8_t qbuf[LQP];
-    __shared__ uint64_t cand[kMaxCands];
-    __shared__ int ncand_s, ncls_s;
+    constexpr int PST = ((LQ + 3) & ~3) + 4; // pair-profile row stride in words (+4: bank spread)
+    __shared__ __align__(16) uint32_t pprof[25 * PST];
+    __shared__ __align__(16) uint8_t qbuf[(LQ + 15) & ~15];
+    __shared__ uint32_t qmask[8]; // bytes present in the query
+    __shared__ uint32_t cand[kMaxCands];
+    __shared__ int ncand_s, flag_s;
 
     const int tid = threadIdx.x; // one wave per workgroup
     const int lane = tid & 63;
@@ -383,13 +384,14 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 const bool keep = id < (uint64_t)a.n_ref;
                 const uint64_t m = __ballot(keep);
                 if (keep)
-                    cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = id;
+                    cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = (uint32_t)id;
                 base += __popcll(m);
             }
             if (tid == 0)
                 ncand_s = base;
         } else if (tid == 0) {
-            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride), duplicates kept
+            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride); the expansion
+            // is mapped back to the original count (:502-507), so duplicates are kept
             int nc = 0;
             bool overflow = false;
             for (int i = 0; i < nsel && !overflow; ++i) {
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                         if (nc >= kMaxCands)
                             overflow = true;
                         else
-                            cand[nc++] = id;
+                            cand[nc++] = (uint32_t)id;
                     }
                     continue;
                 }
@@ -414,47 +416,32 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                         overflow = true;
                         break;
                     }
-                    cand[nc++] = pos;
+                    cand[nc++] = (uint32_t)pos;
                 }
             }
             ncand_s = overflow ? -2 : nc;
         }
-        for (int t = tid; t < LQP; t += 64)
+        for (int t = tid; t < ((LQ + 15) & ~15); t += 64)
             qbuf[t] = (t < qlen && t < LQ) ? a.queries[q * a.q_stride + t] : 0;
-        reinterpret_cast<uint32_t *>(cls_map)[tid] = 0u;
-        __syncthreads();
-        if (tid == 0) { // classes in first-occurrence order
-            int ncls = 0;
-            for (int j = 0; j < qlen && j < LQ; ++j) {
-                const int b = qbuf[j];
-                if (cls_map[b] == 0) {
-                    if (ncls + 1 >= kNcls) {
-                        ncls = kNcls; // too many distinct bytes: bit-profile kernel
-                        break;
-                    }
-                    cls_map[b] = (uint8_t)(++ncls);
-                }
-            }
-            ncls_s = ncls;
-        }
-        __syncthreads();
-        for (int e = tid; e < kNcls * LQP / 4; e += 64) {
-            const int c = e / (LQP / 4), j0 = (e % (LQP / 4)) * 4;
-            uint32_t word = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u;
-                if (c > 0 && j < qlen && j < LQ && cls_map[qbuf[j]] == c)
-                    word |= 0x18u << (8 * u);
-            }
-            reinterpret_cast<uint32_t *>(cprof)[e] = word;
-        }
-        __syncthreads();
-        int ncand = (qlen > LQ) ? -3 : ncand_s;
-        if (ncand >= 0 && ncls_s >= kNcls)
-            ncand = kNeedBitProfile;
+        if (tid < 8)
+            qmask[tid] = 0u;
         if (tid == 0)
-            a.ncand[q] = ncand;
+            flag_s = 0;
+        __syncthreads();
+        for (int t = tid; t < qlen && t < LQ; t += 64)
+            atomicOr(&qmask[qbuf[t] >> 5], 1u << (qbuf[t] & 31));
+        for (int e = tid; e < 25 * PST; e += 64) {
+            const int combo = e / PST, j = e % PST;
+            uint32_t word = 0;
+            if (j < qlen && j < LQ) {
+                const int c = qbuf[j];
+                word = (c == acgt_byte(combo / 5) ? 0x1800u : 0u) | (c == acgt_byte(combo % 5) ? 0x18000000u : 0u);
+            }
+            pprof[e] = word;
+        }
+        __syncthreads();
+        const int ncand = (qlen > LQ) ? -3 : ncand_s;
+        bool flagged = false;
         // two candidates per lane: c and c + 64
         for (int c0 = tid; c0 < ncand; c0 += 128) {
             const int c1 = c0 + 64;
@@ -464,22 +451,28 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             for (int j = 0; j < LQ; ++j)
                 H[j] = (h2){(_Float16)0.0f, (_Float16)0.0f};
             h2 best = {(_Float16)0.0f, (_Float16)0.0f};
-            const uint64_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
+            const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
             const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
             const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
             const int L = a.ref_len;
-            int na = (L > 0) ? (int)pa[0] : -1;
-            int nb2 = (L > 0 && has_b) ? (int)pb[0] : -1;
+            int na = (L > 0) ? (int)pa[0] : 0;
+            int nb2 = (L > 0) ? (int)pb[0] : 0;
             for (int i = 0; i < L; ++i) {
                 const int ca = na, cb = nb2;
                 if (i + 1 < L) { // prefetch the next row's bytes
                     na = pa[i + 1];
-                    nb2 = has_b ? (int)pb[i + 1] : -1;
+                    nb2 = pb[i + 1];
                 }
-                const int ka = cls_map[ca];
-                const int kb = cb >= 0 ? (int)cls_map[cb] : 0;
-                sw_row_f16<LQ>(H, reinterpret_cast<const uint32_t *>(cprof + ka * LQP),
-                               reinterpret_cast<const uint32_t *>(cprof + kb * LQP), best);
+                int ka = acgt_code(ca), kb = acgt_code(cb);
+                if (ka < 0) {
+                    flagged |= ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
+                    ka = 4;
+                }
+                if (kb < 0) {
+                    flagged |= has_b && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
+                    kb = 4;
+                }
+                sw_row_f16<LQ>(H, pprof + (ka * 5 + kb) * PST, best);
             }
             a.cand_ids[q * a.cmax + c0] = wa;
             a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);
@@ -488,6 +481,11 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 a.cand_scores[q * a.cmax + c1] = (int32_t)((float)best.y * 1024.0f);
             }
         }
+        if (__ballot(flagged) != 0ull && lane == 0)
+            flag_s = 1;
+        __syncthreads();
+        if (tid == 0)
+            a.ncand[q] = (ncand >= 0 && flag_s) ? kNeedBitProfile : ncand;
         __syncthreads();
     }
 }
@@ -613,8 +611,8 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     a.cand_scores = refs.ws_scores;
     a.ncand = refs.ws_ncand;
     const int grid = (int)std::min<int64_t>(a.nq, 65536);
-    // fp16 class-profile kernel first; the bit-profile kernel then scores only the queries it flagged
-    // (more than kNcls-1 distinct bytes). DRM_SW_BITPROFILE=1 forces the bit-profile kernel.
+    // fp16 pair-profile kernel for queries up to 152 bytes; the bit-profile kernel re-scores the
+    // queries it flagged, and takes longer queries (or everything when DRM_SW_BITPROFILE=1).
     static const bool force_bits = [] {
         const char *e = std::getenv("DRM_SW_BITPROFILE");
         return e && std::atoi(e) != 0;
