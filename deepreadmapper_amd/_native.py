@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdrm_hip.so")
+# DRM_LIB selects another in-tree build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("DRM_LIB") or os.path.join(_HERE, "libdrm_hip.so")
 
 DRM_OK = 0
 DRM_ERR_ARG = -1
