@@ -223,6 +223,8 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.vmode = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_EXACT"))
             d.force_exact = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
+            d.waves_per_cu = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
             d.try_sorted = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))

@@ -30,6 +30,7 @@ struct DeviceIndex {
     int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
     int32_t force_exact = 0;   // skip the sorted-array pass (every query through the exact kernel)
     int32_t try_sorted = 0;    // run the sorted-array pass first (DRM_SEARCH_SORTED=1)
+    int32_t waves_per_cu = 20; // resident search waves per CU (LDS allows 20 at 8 KB of LUT each)
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
@@ -76,6 +77,7 @@ struct SearchArgs {
     int32_t clear_cap;
     uint32_t *counter;
     int32_t check_dups;
+    int32_t x_aligned16; // queries 16-B aligned: float4 loads in the LUT build
     uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1), else null
     const int32_t *qlist;  // exact kernel, fallback pass: process qlist[0 .. *qcount) instead of 0 .. n
     const uint32_t *qcount;

@@ -378,14 +378,30 @@ struct PairHeap {
         const bool takeL = (lane == 63) || (2 * lane + 3 == k + 1) || cmp2(kL, kR, (int32_t)iL, (int32_t)iR);
         const uint64_t lm = __ballot(takeL);
         const uint32_t mk = takeL ? kL : kR, mi = takeL ? iL : iR;
-        int leaf = 1, depth = 0;
-        while (2 * leaf <= k) {
-            leaf = 2 * leaf + (int)(((lm >> (leaf - 1)) & 1ull) ^ 1ull);
-            ++depth;
+        (void)lm;
+        // The max-child path by pointer doubling (VALU + ds_bpermute instead of a scalar walk):
+        // N1(p) = chosen child slot of node slot p (p itself once p has no children; slots >= 64
+        // are leaves), N2 = N1.N1, N4 = N2.N2; lane d then composes its depth-d node from d's bits.
+        const int n1 = (2 * lane + 2 <= k) ? (takeL ? 2 * lane + 1 : 2 * lane + 2) : lane;
+        const int n1n1 = __shfl(n1, n1 & 63, 64);
+        const int n2 = (n1 < 64) ? n1n1 : n1;
+        const int n2n2 = __shfl(n2, n2 & 63, 64);
+        const int n4 = (n2 < 64) ? n2n2 : n2;
+        const int root_child = __builtin_amdgcn_readlane(n1, 0); // explicit lane (readfirstlane would follow exec)
+        int sd = (lane & 1) ? root_child : 0;
+        {
+            const int t = __shfl(n2, sd & 63, 64);
+            sd = ((lane & 2) && sd < 64) ? t : sd;
+            const int u = __shfl(n4, sd & 63, 64);
+            sd = ((lane & 4) && sd < 64) ? u : sd;
         }
+        // sd = 0-based path slot at depth `lane` (lanes 0..7); the previous depth's via DPP row_shr:1
+        const int sprev = (int)dpp_u32(0u, (uint32_t)sd, 0x111, 0xF);
+        const int depth = __popcll(__ballot(lane >= 1 && lane <= 7 && sd != sprev));
+        const int leaf = __builtin_amdgcn_readlane(sd, 7) + 1; // 1-based
         // lane l in [1, depth]: the path node at depth l = the chosen child of the node above it
         const bool onpath = lane >= 1 && lane <= depth;
-        const int par = onpath ? (leaf >> (depth - lane + 1)) - 1 : 0;
+        const int par = onpath ? sprev : 0;
         const uint32_t ak = (uint32_t)__shfl((int)mk, par, 64), ai = (uint32_t)__shfl((int)mi, par, 64);
         const int h = __builtin_ctzll(__ballot(lane >= 1 && (!onpath || cmp2(vk, ak, vi, (int32_t)ai)))) - 1;
         // depth m takes depth m+1's value for m < h; depth h takes the sifted element
@@ -456,14 +472,14 @@ template <bool FAST8> __device__ __forceinline__ uint2 load_code8(const SearchAr
     return make_uint2(0u, 0u);
 }
 
-// set_query: qv <- x[q], LUT[m][c] = sum_t (x - c)^2 over the sub-vector, sequential t, no FMA
-// (PQDistanceComputer::set_query -> compute_distance_table) [upstream faiss]
-__device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float *lut, float *qv, int lane)
+// set_query: LUT[m][c] = sum_t (x - c)^2 over the sub-vector, sequential t, no FMA
+// (PQDistanceComputer::set_query -> compute_distance_table) [upstream faiss]. The query is read
+// straight from global memory (every lane of a pass reads the same 64 B: one L1 broadcast), so the
+// only LDS a wave owns is its LUT -- 8 KB, i.e. 20 resident waves per CU.
+__device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float *lut, int lane)
 {
-    for (int t = lane; t < a.d; t += 64)
-        qv[t] = a.x[(int64_t)q * a.d + t];
-    __syncthreads();
-    if (a.dsub == 16 && (a.ksub & 127) == 0) {
+    const float *qv = a.x + q * a.d;
+    if (a.dsub == 16 && (a.ksub & 127) == 0 && a.x_aligned16) {
         // 2 entries of one sub-quantizer per lane per pass, 8 float4 loads in flight
         for (int e0 = lane; e0 < a.M * a.ksub; e0 += 128) {
             const int m = e0 / a.ksub;
@@ -587,8 +603,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
-    float *qv = lut + a.M * a.ksub;
-    int32_t *ht = reinterpret_cast<int32_t *>(qv + ((a.d + 3) & ~3)); // visited hash (VMODE 1)
+    int32_t *ht = reinterpret_cast<int32_t *>(lut + a.M * a.ksub); // visited hash (VMODE 1)
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     const uint32_t kInfKey = ord32(INFINITY);
@@ -625,7 +640,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             for (int t = lane; t < kHashSlots / 4; t += 64)
                 h4[t] = make_int4(-1, -1, -1, -1);
         }
-        build_lut(a, q, lut, qv, lane);
+        build_lut(a, q, lut, lane);
         DRM_STAMP(0);
         int32_t nearest;
         uint32_t dn;
@@ -968,7 +983,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
-    float *qv = lut + a.M * a.ksub;
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     const uint32_t kInfKey = ord32(INFINITY);
@@ -996,7 +1010,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             continue;
         }
         DRM_STAMP(7);
-        build_lut(a, q, lut, qv, lane);
+        build_lut(a, q, lut, lane);
         DRM_STAMP(0);
         int32_t nearest;
         uint32_t dn;
@@ -1225,13 +1239,13 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     }
     const int vmode = ix.vmode;
     const size_t scratch = vmode == 1 ? sizeof(int32_t) * 2048 : 0;
-    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub + sizeof(float) * (size_t)((ix.d + 3) & ~3) + scratch;
+    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub + scratch; // LUT, [hash]
     if (lds > 160 * 1024)
         throw Error(DRM_ERR_UNSUPPORTED, "search workspace does not fit in LDS");
 
     int cus = 0;
     DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
-    int per_cu = std::max(1, std::min(16, (int)((160 * 1024) / lds)));
+    int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
     // (re)allocate per-slot workspace
     const int64_t words = (ix.ntotal + 31) / 32;
@@ -1289,6 +1303,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.counter = ix.counter;
     a.check_dups = ix.has_dup_links;
     a.stamps = ix.stamps;
+    a.x_aligned16 = ((uintptr_t)d_x % 16) == 0;
 
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
     // The sorted-array pass only pays off when distance ties are rare; stride-1 genome windows

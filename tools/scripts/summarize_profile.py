@@ -20,7 +20,7 @@ if os.path.exists(stats):
         js["kernels"].setdefault(r["Name"], {})["avg_ms"] = float(r["AverageNs"]) / 1e6
         js["kernels"][r["Name"]]["calls"] = int(r["Calls"])
 out.append("## PMC (per dispatch averages)")
-for f in sorted(glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv"))):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f)):
