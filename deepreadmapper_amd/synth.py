@@ -125,10 +125,13 @@ class Workload:
         self.name, self.genome_len, self.n_queries = name, genome_len, n_queries
         self.ref_len, self.stride, self.seed, self.read_seed, self.sub_rate = ref_len, stride, seed, read_seed, sub_rate
 
-    def generate(self, workdir, efc=200, M_hnsw=16, M_pq=8, nbits=8, nthreads=0, build_seed=0, log=None):
+    def generate(self, workdir, efc=200, M_hnsw=16, M_pq=8, nbits=8, nthreads=0, build_seed=0, log=None,
+                 need_refs=True):
+        """need_refs=False skips the stride-1 window table (search-only workloads such as C4)."""
         os.makedirs(workdir, exist_ok=True)
         self.genome = genome(self.genome_len, self.seed)
-        self.refs = windows_lookup(self.genome, self.ref_len, 1)  # static ref_seqs: stride 1 always
+        # static ref_seqs: stride 1 always
+        self.refs = windows_lookup(self.genome, self.ref_len, 1) if need_refs else None
         self.reads, self.names, self.truth = simulate_reads(self.genome, self.n_queries, self.ref_len,
                                                             self.sub_rate, self.read_seed)
         self.queries = tag(self.reads)
