@@ -60,6 +60,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# The contract is ONE JSON line on stdout. Native libraries (gloo, RCCL) print banners to fd 1, so
+# fd 1 is pointed at stderr for the whole run and the result goes to a saved copy of the original.
+_RESULT_OUT = None
+
+
+def emit(obj):
+    out = _RESULT_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
+def _claim_stdout():
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 class Dist:
     """Control plane for N>1 ranks (barrier, max, sum) over torch.distributed gloo; the data path
     has no collective (queries are independent, the index is replicated per GPU)."""
@@ -69,6 +87,7 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.dist = None
+        self.nccl = None  # RCCL group for the end-of-run result gather
         if self.world > 1:
             import torch.distributed as dist  # imported before libdrm_hip.so is loaded
             dist.init_process_group("gloo")
@@ -119,6 +138,35 @@ def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn):
     return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
             "sample": f"first {n} of this rank's C3 reads (oracle/ C restatement, OpenMP {threads} threads on "
                       f"{cpu_model()}): search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+
+
+def gather_results(D, dev, n_total, bufs, local_host):
+    """End-of-run exchange: every rank's result rows are all-gathered to rank 0 over
+    RCCL (torch.distributed nccl backend, xGMI), outside the timed region, and rank 0 checks its own
+    shard in the gathered arrays. Reported, never fatal: the scaling numbers stand either way."""
+    if D.world == 1:
+        return None
+    try:
+        import torch
+        from deepreadmapper_amd.shard import gather_rows_device
+        torch.cuda.set_device(dev)
+        if D.nccl is None:
+            D.nccl = D.dist.new_group(backend="nccl")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        full = {name: gather_rows_device(b, n_total, D.rank, D.world, D.dist, group=D.nccl) for name, b in bufs}
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        out = {"backend": "nccl (RCCL)", "ms": round(ms, 3),
+               "bytes_per_rank": int(sum(b.nbytes for _, b in bufs))}
+        if D.rank == 0:
+            from deepreadmapper_amd.shard import shard_range
+            lo, hi = shard_range(n_total, 0, D.world)
+            out["rank0_shard_matches"] = bool(all(np.array_equal(full[k][lo:hi], v) for k, v in local_host.items()))
+            out["rows"] = int(full[bufs[0][0]].shape[0])
+        return out
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def run_c4(args, D):
@@ -191,7 +239,7 @@ def run_c4(args, D):
                "sample": f"first {n} C4 queries, oracle search only (OpenMP {threads} threads on {cpu_model()})"}
     if D.rank == 0:
         r = runs[args.k]
-        print(json.dumps({
+        emit({
             "metric": f"searched reads/sec (HNSW-PQ only), EF={args.ef} K={args.k}",
             "value": round(r["value"], 1), "unit": "reads/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(r["ms"], 3), "higher_is_better": True, "scaling": "weak",
@@ -208,7 +256,7 @@ def run_c4(args, D):
             "k5": {"value": round(runs[5]["value"], 1), "ms": round(runs[5]["ms"], 3),
                    "achieved_gbs": round(runs[5]["achieved"], 2)},
             "breakdown": {"ndis_mean": round(r["ndis"], 1), "nhops_mean": round(r["nhops"], 1)},
-        }), flush=True)
+        })
     D.close()
 
 
@@ -228,6 +276,7 @@ def main():
                     help="c3 (default, the headline): search + SW rerank; c4: search only on a 10M-vector "
                          "sparse (stride 4) index, SURVEY.md sec. 8d")
     args = ap.parse_args()
+    _claim_stdout()
 
     D = Dist()
     if args.workload == "c4":
@@ -330,6 +379,8 @@ def main():
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
+    gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_I),
+                                           ("search_dists", d_D)], {"sw_ids": ids})
     result = None
     if D.rank == 0:
         cpu = None
@@ -361,6 +412,7 @@ def main():
                             "valu_issue_frac_pmc": round(sw_pmc["valu_issue_frac"], 3)
                             if sw_pmc and "valu_issue_frac" in sw_pmc else None},
             "cpu_baseline": cpu,
+            "gather": gather,
             "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
@@ -368,7 +420,7 @@ def main():
                           "tie_fallback_queries": n_fallback,
                           "truth_top1": round(top1, 4), "truth_in_topk": round(intop, 4)},
         }
-        print(json.dumps(result), flush=True)
+        emit(result)
     D.close()
 
 

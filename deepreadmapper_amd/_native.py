@@ -23,7 +23,7 @@ DRM_ERR_UNSUPPORTED = -7
 EXPORTS = [
     "drm_last_error", "drm_version", "drm_device_count", "drm_set_device", "drm_device_sync", "drm_malloc",
     "drm_free", "drm_memset", "drm_memcpy_h2d", "drm_memcpy_d2h", "drm_stream_create", "drm_stream_destroy",
-    "drm_stream_sync", "drm_event_create", "drm_event_destroy", "drm_event_record", "drm_event_elapsed_ms",
+    "drm_stream_sync", "drm_event_create", "drm_event_destroy", "drm_event_record", "drm_stream_wait_event", "drm_event_elapsed_ms",
     "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device",
     "drm_search_device_ex", "drm_search_fallbacks", "drm_sw_scores",
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
@@ -79,6 +79,7 @@ def lib():
         "drm_event_create": (C.c_int, [C.POINTER(vp)]),
         "drm_event_destroy": (C.c_int, [vp]),
         "drm_event_record": (C.c_int, [vp, vp]),
+        "drm_stream_wait_event": (C.c_int, [vp, vp]),
         "drm_event_elapsed_ms": (C.c_int, [vp, vp, C.POINTER(C.c_float)]),
         "drm_index_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
         "drm_index_free": (C.c_int, [vp]),

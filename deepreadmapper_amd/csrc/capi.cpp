@@ -154,6 +154,10 @@ int drm_event_record(void *ev, void *stream)
 {
     return guarded([&] { DRM_HIP_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream)); });
 }
+int drm_stream_wait_event(void *stream, void *ev)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0)); });
+}
 int drm_event_elapsed_ms(void *start, void *stop, float *ms)
 {
     return guarded([&] {

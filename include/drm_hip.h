@@ -66,6 +66,8 @@ int drm_stream_sync(void *stream);
 int drm_event_create(void **ev);
 int drm_event_destroy(void *ev);
 int drm_event_record(void *ev, void *stream);
+/* Work enqueued on `stream` after this call waits for `ev` (pipelining search and rerank on two streams). */
+int drm_stream_wait_event(void *stream, void *ev);
 int drm_event_elapsed_ms(void *start, void *stop, float *ms);
 
 /* ---------------------------------------------------------------- index (search side)
