@@ -1,8 +1,10 @@
 """deepreadmapper_amd -- MI355X-native drop-in for DeepReadMapper's query hot path:
-HNSW-PQ candidate search (faiss_search) + Smith-Waterman rerank (post_process_sw_static),
-implemented as HIP kernels for gfx950 behind the C ABI in include/drm_hip.h."""
+HNSW-PQ candidate search (faiss_search), fp32-L2 HNSW search on hnswlib indexes (search), and the
+Smith-Waterman rerank (post_process_sw_static), implemented as HIP kernels for gfx950 behind the C
+ABI in include/drm_hip.h."""
 from ._native import DrmError, lib  # noqa: F401  (ImportError if libdrm_hip.so is missing)
 from .search import HnswPqIndex, faiss_search, read_index  # noqa: F401
+from .flat import HnswFlatIndex, load_flat_index  # noqa: F401  (fp32-L2 hnswlib backend)
 from .rerank import (WindowTable, calc_sw_score, calc_sw_scores, post_process_sw_static,  # noqa: F401
                      rerank_arrays, sw_reranker)
 

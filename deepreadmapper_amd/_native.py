@@ -27,7 +27,9 @@ EXPORTS = [
     "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device",
     "drm_search_device_ex", "drm_search_fallbacks", "drm_sw_scores",
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
-    "drm_build_hnswpq", "drm_embed_kmer3",
+    "drm_build_hnswpq", "drm_build_hnsw_flat", "drm_embed_kmer3",
+    "drm_flat_index_load", "drm_flat_index_free", "drm_flat_index_get_info", "drm_flat_search",
+    "drm_flat_search_device", "drm_flat_search_overflows",
 ]
 
 
@@ -44,6 +46,12 @@ class IndexInfo(C.Structure):
                 ("M_hnsw", C.c_int32), ("max_level", C.c_int32), ("entry_point", C.c_int32),
                 ("efConstruction", C.c_int32), ("efSearch", C.c_int32), ("metric_type", C.c_int32),
                 ("device_bytes", C.c_int64)]
+
+
+class FlatIndexInfo(C.Structure):
+    _fields_ = [("d", C.c_int32), ("ntotal", C.c_int64), ("M", C.c_int32), ("maxM0", C.c_int32),
+                ("maxM", C.c_int32), ("max_level", C.c_int32), ("entry_point", C.c_uint32),
+                ("efConstruction", C.c_int32), ("device_bytes", C.c_int64)]
 
 
 class SearchStats(C.Structure):
@@ -97,6 +105,13 @@ def lib():
                                                         vp]),
         "drm_build_hnswpq": (C.c_int, [vp, i64, i32, i32, i32, i32, i32, C.c_double, i32, C.c_uint64,
                                        C.c_char_p]),
+        "drm_flat_index_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
+        "drm_flat_index_free": (C.c_int, [vp]),
+        "drm_flat_index_get_info": (C.c_int, [vp, C.POINTER(FlatIndexInfo)]),
+        "drm_flat_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
+        "drm_flat_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
+        "drm_flat_search_overflows": (C.c_int, [vp, C.POINTER(i64)]),
+        "drm_build_hnsw_flat": (C.c_int, [vp, i64, i32, i32, i32, i32, C.c_uint64, C.c_char_p]),
         "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),
     }
     for name, (res, args) in sigs.items():

@@ -21,6 +21,9 @@ struct drm_index {
 struct drm_refs {
     drm::DeviceRefs dev;
 };
+struct drm_flat_index {
+    drm::DeviceFlatIndex dev;
+};
 
 using drm::Error;
 
@@ -380,6 +383,182 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
         (void)hipEventDestroy(e1);
         dD.download(D);
         dI.download(I);
+        if (stats) {
+            std::vector<int32_t> st((size_t)n * 2);
+            dst.download(st.data());
+            stats->nq = n;
+            stats->ndis = std::accumulate(st.begin(), st.begin() + n, (int64_t)0);
+            stats->nhops = std::accumulate(st.begin() + n, st.end(), (int64_t)0);
+            stats->kernel_ms = ms;
+        }
+    });
+}
+
+// ------------------------------------------------------------------------ fp32 (hnswlib) index
+namespace {
+void free_flat(drm::DeviceFlatIndex &d)
+{
+    void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,  d.up, d.labels,
+                    d.visited,    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.counter};
+    for (void *p : ptrs)
+        if (p)
+            (void)hipFree(p);
+}
+} // namespace
+
+int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
+{
+    return guarded([&] {
+        if (!path || !out)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *out = nullptr;
+        drm::HnswFlatHost h = drm::read_hnswlib(path);
+        if (h.d % 16 != 0)
+            throw Error(DRM_ERR_UNSUPPORTED, "fp32 GPU search needs d % 16 == 0 (hnswlib L2SqrSIMD16Ext)");
+        if (h.maxM0 > 4096 || h.maxM > 4096)
+            throw Error(DRM_ERR_UNSUPPORTED, "maxM0/maxM > 4096");
+        if (h.n > 0xFFFFFFFFll)
+            throw Error(DRM_ERR_UNSUPPORTED, "more than 2^32 elements");
+        DRM_HIP_CHECK(hipSetDevice(device));
+        std::unique_ptr<drm_flat_index, void (*)(drm_flat_index *)> ix(new drm_flat_index(), [](drm_flat_index *p) {
+            free_flat(p->dev);
+            delete p;
+        });
+        drm::DeviceFlatIndex &d = ix->dev;
+        d.device = device;
+        d.d = h.d;
+        d.ntotal = h.n;
+        d.maxM0 = (int32_t)h.maxM0;
+        d.maxM = (int32_t)h.maxM;
+        d.M = (int32_t)h.M;
+        d.efc = (int32_t)h.efc;
+        d.maxlevel = h.maxlevel;
+        d.ep = h.ep;
+        const int64_t n = h.n;
+        std::vector<uint32_t> l0((size_t)n * d.maxM0, 0u), cnt((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t *row = &h.l0[(size_t)i * (1 + h.maxM0)];
+            cnt[(size_t)i] = row[0] & 0xFFFFu;
+            std::memcpy(&l0[(size_t)i * d.maxM0], row + 1, sizeof(uint32_t) * d.maxM0);
+            if (!d.has_dup_links) { // a row listing one id twice: only its first occurrence is fresh
+                std::unordered_set<uint32_t> seen;
+                for (uint32_t j = 0; j < cnt[(size_t)i]; ++j)
+                    if (!seen.insert(row[1 + j]).second) {
+                        d.has_dup_links = 1;
+                        break;
+                    }
+            }
+        }
+        if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
+            d.waves_per_cu = std::max(1, std::atoi(e));
+        d.vec = upload_vec(h.vec, d.device_bytes);
+        d.l0 = upload_vec(l0, d.device_bytes);
+        d.l0cnt = upload_vec(cnt, d.device_bytes);
+        d.up_off = upload_vec(h.up_off, d.device_bytes);
+        d.up = upload_vec(h.up.empty() ? std::vector<uint32_t>(1, 0u) : h.up, d.device_bytes);
+        d.labels = upload_vec(h.labels, d.device_bytes);
+        h.vec.clear();
+        h.vec.shrink_to_fit();
+        h.l0.clear();
+        h.l0.shrink_to_fit();
+        h.up.clear();
+        h.up.shrink_to_fit();
+        d.meta = std::move(h);
+        *out = ix.release();
+    });
+}
+
+int drm_flat_index_free(drm_flat_index *index)
+{
+    return guarded([&] {
+        if (!index)
+            return;
+        free_flat(index->dev);
+        delete index;
+    });
+}
+
+int drm_flat_index_get_info(const drm_flat_index *index, drm_flat_index_info *info)
+{
+    return guarded([&] {
+        if (!index || !info)
+            throw Error(DRM_ERR_ARG, "null argument");
+        const drm::DeviceFlatIndex &d = index->dev;
+        info->d = d.d;
+        info->ntotal = d.ntotal;
+        info->M = d.M;
+        info->maxM0 = d.maxM0;
+        info->maxM = d.maxM;
+        info->max_level = d.maxlevel;
+        info->entry_point = d.ep;
+        info->efConstruction = d.efc;
+        info->device_bytes = d.device_bytes;
+    });
+}
+
+int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, void *stream)
+{
+    return guarded([&] {
+        if (!index || (n > 0 && (!d_x || !d_D || !d_labels || !d_ndis || !d_nhops)))
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (n <= 0)
+            throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswlib_dir/search.cpp:20-23
+        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
+        drm::launch_hnsw_flat_search(index->dev, d_x, n, k, ef, d_D, d_labels, d_ndis, d_nhops,
+                                     (hipStream_t)stream);
+    });
+}
+
+int drm_flat_search_overflows(drm_flat_index *index, int64_t *count)
+{
+    return guarded([&] {
+        if (!index || !count)
+            throw Error(DRM_ERR_ARG, "null argument");
+        uint32_t c[2] = {0, 0};
+        if (index->dev.counter) {
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+        }
+        *count = (int64_t)c[1];
+    });
+}
+
+int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d, int32_t k, int32_t ef, float *D,
+                    uint64_t *labels, drm_search_stats *stats)
+{
+    return guarded([&] {
+        if (!index || !x || !D || !labels)
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (n <= 0)
+            throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswlib_dir/search.cpp:20-23
+        if (d != index->dev.d)
+            throw Error(DRM_ERR_ARG, "query dimension " + std::to_string(d) + " != index dimension " +
+                                         std::to_string(index->dev.d));
+        if (k <= 0)
+            throw Error(DRM_ERR_ARG, "k must be > 0");
+        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
+        DevBuf<float> dx((size_t)n * d), dD((size_t)n * k);
+        DevBuf<uint64_t> dL((size_t)n * k);
+        DevBuf<int32_t> dst((size_t)n * 2);
+        dx.upload(x);
+        hipEvent_t e0, e1;
+        DRM_HIP_CHECK(hipEventCreate(&e0));
+        DRM_HIP_CHECK(hipEventCreate(&e1));
+        DRM_HIP_CHECK(hipEventRecord(e0, nullptr));
+        drm::launch_hnsw_flat_search(index->dev, dx.p, n, k, ef, dD.p, dL.p, dst.p, dst.p + n, nullptr);
+        DRM_HIP_CHECK(hipEventRecord(e1, nullptr));
+        DRM_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        DRM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        uint32_t c[2] = {0, 0};
+        DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+        if (c[1])
+            throw Error(DRM_ERR_UNSUPPORTED, std::to_string(c[1]) + " queries outgrew the GPU candidate heap");
+        dD.download(D);
+        dL.download(labels);
         if (stats) {
             std::vector<int32_t> st((size_t)n * 2);
             dst.download(st.data());

@@ -90,6 +90,68 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
 void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                             int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 
+// ---------------------------------------------------------------------- fp32 (hnswlib) index
+// HBM image of an hnswlib HierarchicalNSW<float> (DESIGN.md "fp32 mode").
+struct DeviceFlatIndex {
+    int device = 0;
+    int32_t d = 0, maxM0 = 0, maxM = 0, maxlevel = -1, M = 0, efc = 0;
+    uint32_t ep = 0;
+    int64_t ntotal = 0;
+    int32_t has_dup_links = 0;
+    int32_t waves_per_cu = 20;
+    float *vec = nullptr;      // [ntotal][d] f32 (512-B rows at d = 128)
+    uint32_t *l0 = nullptr;    // [ntotal][maxM0] level-0 links (512-B rows at maxM0 = 128)
+    uint32_t *l0cnt = nullptr; // [ntotal] link counts
+    int64_t *up_off = nullptr; // [ntotal] first word of the node's upper blocks, -1 if none
+    uint32_t *up = nullptr;    // blocks of (1 + maxM) words: count, links
+    uint64_t *labels = nullptr;
+    // search workspace (per resident wave slot), grown on demand
+    int32_t n_slots = 0;
+    int64_t vis_words = 0;
+    uint32_t *visited = nullptr;
+    int32_t clear_cap = 0;
+    int32_t *clear_list = nullptr;
+    int64_t cand_ovf_cap = 0;       // candidate_set entries beyond the LDS part, per slot
+    float *cand_ovf_k = nullptr;
+    uint32_t *cand_ovf_i = nullptr;
+    uint32_t *counter = nullptr;    // [0] work queue head, [1] candidate_set overflows
+    int64_t device_bytes = 0;
+    HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
+};
+
+struct FlatArgs {
+    const float *x;
+    int64_t n;
+    int32_t d;
+    const float *vec;
+    const uint32_t *l0;
+    const uint32_t *l0cnt;
+    int32_t maxM0;
+    const int64_t *up_off;
+    const uint32_t *up;
+    int32_t maxM, maxlevel;
+    uint32_t ep;
+    int64_t ntotal;
+    const uint64_t *labels;
+    int32_t k, ef;
+    float *D;
+    uint64_t *L;
+    int32_t *ndis, *nhops;
+    uint32_t *visited;
+    int64_t vis_words;
+    int32_t *clear_list;
+    int32_t clear_cap;
+    uint32_t *counter;
+    int32_t check_dups;
+    int32_t cand_lds;
+    float *cand_ovf_k;
+    uint32_t *cand_ovf_i;
+    int64_t cand_ovf_cap;
+};
+
+void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,
+                             uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream);
+
 // ---------------------------------------------------------------------------------- SW rerank
 struct DeviceRefs {
     int device = 0;

@@ -63,6 +63,29 @@ HnswPqHost read_hnswpq(const std::string &path);                 // throws Error
 void write_hnswpq(const HnswPqHost &ix, const std::string &path); // throws Error
 void validate_hnswpq(const HnswPqHost &ix);                      // throws Error(DRM_ERR_FORMAT)
 
+// ---------------------------------------------------------------------------------------------
+// Host image of an hnswlib HierarchicalNSW<float> file (saveIndex/loadIndex, hnswlib_io.cpp):
+// the reference's fp32-L2 backend (src/hnswlib_dir/*).
+// ---------------------------------------------------------------------------------------------
+struct HnswFlatHost {
+    int32_t d = 0;
+    int64_t n = 0;
+    uint64_t max_elements = 0, maxM = 0, maxM0 = 0, M = 0, efc = 0;
+    int32_t maxlevel = -1;
+    uint32_t ep = 0;
+    double mult = 0.0;
+    std::vector<float> vec;       // [n][d]
+    std::vector<uint32_t> l0;     // [n][1 + maxM0]: header (count in low 16 bits), links
+    std::vector<uint64_t> labels; // [n]
+    std::vector<int32_t> levels;  // [n]
+    std::vector<int64_t> up_off;  // [n]: first word of the node's upper blocks in `up`, -1 if none
+    std::vector<uint32_t> up;     // blocks of (1 + maxM) words, block l-1 = level l
+};
+HnswFlatHost read_hnswlib(const std::string &path);                  // throws Error
+void write_hnswlib(const HnswFlatHost &ix, const std::string &path); // throws Error
+void build_hnsw_flat(const float *x, int64_t n, int d, int M, int efc, int nthreads, uint64_t seed,
+                     const std::string &path);
+
 // faiss HNSW::set_default_probas(M, 1/log(M)) [faiss impl/HNSW.cpp]
 void hnsw_default_probas(int M, std::vector<double> &probas, std::vector<int32_t> &cum);
 

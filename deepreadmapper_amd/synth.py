@@ -103,6 +103,14 @@ def build_index(x, path, M_pq=8, nbits=8, M_hnsw=16, efc=200, sample_rate=0.5, n
                                  C.c_uint64(seed), str(path).encode()))
 
 
+def build_flat_index(x, path, M=64, efc=128, nthreads=0, seed=0):
+    """hnswlib build_index back end (src/hnswlib_dir/index.cpp:3-49) -> hnswlib file (fp32 L2)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    check(lib().drm_build_hnsw_flat(ptr(x), x.shape[0], x.shape[1], M, efc, nthreads, C.c_uint64(seed),
+                                    str(path).encode()))
+
+
 def write_fasta(path, g, header="> Synthetic genome", width=80):
     g = bytes(np.asarray(g, dtype=np.uint8))
     with open(path, "wb") as f:

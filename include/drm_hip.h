@@ -100,6 +100,40 @@ int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t 
  * exact distance tie and were re-run by the exact (faiss heap-layout) kernel. Synchronizes the device. */
 int drm_search_fallbacks(drm_index *index, int64_t *count);
 
+/* ---------------------------------------------------------------- fp32-L2 index (hnswlib)
+ * The reference's hnswlib backend (BASELINE configs[1] "HIP L2 HNSW
+ * search"): an hnswlib HierarchicalNSW<float> file searched with fp32 squared-L2 distances. */
+typedef struct drm_flat_index drm_flat_index;
+
+typedef struct {
+    int32_t d;
+    int64_t ntotal;
+    int32_t M, maxM0, maxM; /* hnswlib M_, maxM0_ (level 0), maxM_ (levels >= 1) */
+    int32_t max_level;
+    uint32_t entry_point;
+    int32_t efConstruction;
+    int64_t device_bytes;
+} drm_flat_index_info;
+
+/* new hnswlib::HierarchicalNSW<float>(&space, index_file) (src/hnswlib_dir/test_search.cpp:33):
+ * parses and validates an hnswlib saveIndex file, uploads it to `device`. */
+int drm_flat_index_load(const char *path, int device, drm_flat_index **out);
+int drm_flat_index_free(drm_flat_index *index);
+int drm_flat_index_get_info(const drm_flat_index *index, drm_flat_index_info *info);
+
+/* search(index, query_data, k, ef) (src/hnswlib_dir/search.cpp:7-52, includes/hnswlib_dir/search.hpp):
+ * setEf(ef) then searchKnnCloserFirst(q, k) per query. x: [n][d] f32 host; outputs caller-owned
+ * [n][k]: D = squared L2 ascending, labels = hnswlib labels (u64); a short result is padded with
+ * (+inf, 2^64-1). Throws "Query data is empty" (-1) for n == 0 (search.cpp:20-23). */
+int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d, int32_t k, int32_t ef, float *D,
+                    uint64_t *labels, drm_search_stats *stats);
+/* Same on device buffers, enqueued on `stream`; d_ndis/d_nhops [n] receive per-query counts. */
+int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
+                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, void *stream);
+/* Diagnostic: queries of the last search whose candidate_set outgrew the GPU heap (their outputs
+ * are invalid; drm_flat_search reports it as an error). Synchronizes the device. */
+int drm_flat_search_overflows(drm_flat_index *index, int64_t *count);
+
 /* ---------------------------------------------------------------- Smith-Waterman rerank */
 /* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):
  * pair p scores s1[off1[p] .. +len1[p]) against s2[off2[p] .. +len2[p]). Host pointers. */
@@ -142,6 +176,13 @@ int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors
 int drm_build_hnswpq(const float *x, int64_t n, int32_t d, int32_t M_pq, int32_t nbits, int32_t M_hnsw,
                      int32_t efConstruction, double sample_rate, int32_t nthreads, uint64_t seed,
                      const char *index_path);
+
+/* build_index (src/hnswlib_dir/index.cpp:3-49): hnswlib HierarchicalNSW<float>(L2Space(d), n, M,
+ * efConstruction), addPoint(x[i], label i) for all i, saveIndex -> an hnswlib file (the reference's
+ * defaults: M = Config::Build::GPH_DEG = 64, EFC = 128, includes/utils/config.hpp:30-31). The graph
+ * follows hnswlib's construction algorithm; it need not equal hnswlib's bit for bit. */
+int drm_build_hnsw_flat(const float *x, int64_t n, int32_t d, int32_t M, int32_t efConstruction, int32_t nthreads,
+                        uint64_t seed, const char *index_path);
 
 /* ---------------------------------------------------------------- synthetic embedder
  * Stand-in for the OpenVINO read encoder (Vectorizer::vectorize, src/inference/vectorize.cpp:34-141,

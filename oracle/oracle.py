@@ -9,6 +9,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
 _stl = None
 _ref = None
+_hl = None
 
 
 def _p(a, t):
@@ -151,3 +152,39 @@ def pq_distance_table(fx_or_struct, x):
     lut = np.empty(s.pq_M * s.ksub, dtype=np.float32)
     lib().oracle_pq_distance_table(C.byref(s), _p(x, C.c_float), _p(lut, C.c_float))
     return lut.reshape(s.pq_M, s.ksub)
+
+
+def hnswlib_lib():
+    global _hl
+    if _hl is None:
+        _hl = C.CDLL(os.path.join(_HERE, "libhnswlib_oracle.so"))
+        _hl.oracle_hnswlib_search.restype = C.c_int
+        _hl.oracle_l2_avx.restype = C.c_float
+        _hl.oracle_l2_avx.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    return _hl
+
+
+def l2_avx(x, y):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.ascontiguousarray(y, dtype=np.float32)
+    return float(hnswlib_lib().oracle_l2_avx(x.ctypes.data, y.ctypes.data, int(x.size)))
+
+
+def hnswlib_search(fx, q, k, ef, nthreads=0):
+    """hnswlib searchKnnCloserFirst per query (src/hnswlib_dir/search.cpp:7-52) on a parsed index
+    (oracle/hnswlib_file.read). Returns (D [n,k] f32, I [n,k] i64 labels, ndis, nhops)."""
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    n = q.shape[0]
+    D = np.empty((n, k), dtype=np.float32)
+    I = np.empty((n, k), dtype=np.int64)
+    nd = np.empty(n, dtype=np.int32)
+    nh = np.empty(n, dtype=np.int32)
+    vp = C.c_void_p
+    rc = hnswlib_lib().oracle_hnswlib_search(
+        C.c_int(fx["d"]), C.c_int64(fx["n"]), C.c_int(fx["maxM0"]), C.c_int(fx["maxM"]), C.c_int(fx["maxlevel"]),
+        C.c_uint32(fx["ep"]), vp(fx["vec"].ctypes.data), vp(fx["l0"].ctypes.data), vp(fx["up_off"].ctypes.data),
+        vp(fx["up"].ctypes.data), vp(fx["labels"].ctypes.data), vp(q.ctypes.data), C.c_int64(n), C.c_int(k),
+        C.c_int(ef), vp(D.ctypes.data), vp(I.ctypes.data), vp(nd.ctypes.data), vp(nh.ctypes.data),
+        C.c_int(nthreads))
+    assert rc == 0
+    return D, I, nd, nh

@@ -65,3 +65,37 @@ def repeats(tmp_path_factory):
     reads, _, _ = synth.simulate_reads(g, 300, seed=13)
     q = np.concatenate([synth.embed(synth.tag(reads)), x[::29]])  # plus exact window embeddings
     return {"index": path, "fx": faiss_file.read(path), "x": x, "q": np.ascontiguousarray(q)}
+
+
+def _flat(tmp_path_factory, name, x, M, efc=128):
+    from deepreadmapper_amd import synth
+    from oracle import hnswlib_file
+    d = tmp_path_factory.mktemp(name)
+    path = str(d / f"{name}.hnsw")
+    synth.build_flat_index(x, path, M=M, efc=efc, nthreads=4)
+    return path, hnswlib_file.read(path)
+
+
+@pytest.fixture(scope="session")
+def c1_flat(tmp_path_factory, c1):
+    """C1 windows in an hnswlib fp32 index at the reference's defaults (M = 64, EFC = 128)."""
+    path, fx = _flat(tmp_path_factory, "c1flat", c1["x"], 64)
+    return {"index": path, "fx": fx, "q": c1["q"], "x": c1["x"]}
+
+
+@pytest.fixture(scope="session")
+def syn_flat(tmp_path_factory, syn20k):
+    """The 20k-window synthetic set in an hnswlib fp32 index (M = 16: deeper graph, more hops)."""
+    from oracle import hnswlib_file  # noqa: F401
+    w = syn20k["w"]
+    from deepreadmapper_amd import synth
+    x = synth.embed(synth.tag(synth.windows_lookup(w.genome, 150, 1)))
+    path, fx = _flat(tmp_path_factory, "synflat", x, 16, efc=64)
+    return {"index": path, "fx": fx, "q": w.q_emb, "x": x}
+
+
+@pytest.fixture(scope="session")
+def rep_flat(tmp_path_factory, repeats):
+    """Tie-heavy fp32 index: repeated genome segments give identical vectors, i.e. equal distances."""
+    path, fx = _flat(tmp_path_factory, "repflat", repeats["x"], 32)
+    return {"index": path, "fx": fx, "q": repeats["q"], "x": repeats["x"]}
