@@ -398,8 +398,8 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
 namespace {
 void free_flat(drm::DeviceFlatIndex &d)
 {
-    void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,  d.up, d.labels,
-                    d.visited,    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.counter};
+    void *ptrs[] = {d.vec,     d.l0,         d.l0cnt,      d.up_off,     d.up,        d.labels,   d.visited,
+                    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);

@@ -114,6 +114,9 @@ struct DeviceFlatIndex {
     int64_t cand_ovf_cap = 0;       // candidate_set entries beyond the LDS part, per slot
     float *cand_ovf_k = nullptr;
     uint32_t *cand_ovf_i = nullptr;
+    int64_t top_ovf_cap = 0;        // top_candidates entries beyond the LDS part (large ef), per slot
+    float *top_ovf_k = nullptr;
+    uint32_t *top_ovf_i = nullptr;
     uint32_t *counter = nullptr;    // [0] work queue head, [1] candidate_set overflows
     int64_t device_bytes = 0;
     HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
@@ -147,6 +150,10 @@ struct FlatArgs {
     float *cand_ovf_k;
     uint32_t *cand_ovf_i;
     int64_t cand_ovf_cap;
+    int32_t top_lds;
+    float *top_ovf_k;
+    uint32_t *top_ovf_i;
+    int64_t top_ovf_cap;
 };
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,

@@ -136,17 +136,18 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
-    float *q = reinterpret_cast<float *>(smem);                     // [d]
-    float *topk = q + a.d;                                          // [ef + 1]
-    uint32_t *topi = reinterpret_cast<uint32_t *>(topk + a.ef + 1); // [ef + 1]
-    float *cdk = reinterpret_cast<float *>(topi + a.ef + 1);        // [cand_lds]
+    float *q = reinterpret_cast<float *>(smem);                      // [d]
+    float *topk = q + a.d;                                           // [top_lds]
+    uint32_t *topi = reinterpret_cast<uint32_t *>(topk + a.top_lds); // [top_lds]
+    float *cdk = reinterpret_cast<float *>(topi + a.top_lds);        // [cand_lds]
     uint32_t *cdi = reinterpret_cast<uint32_t *>(cdk + a.cand_lds); // [cand_lds]
     uint32_t *fid = cdi + a.cand_lds;                               // [maxM0] fresh ids / upper links
     float *fd = reinterpret_cast<float *>(fid + a.maxM0);           // [maxM0] their distances
     int *sh = reinterpret_cast<int *>(fd + a.maxM0);                // [4] broadcast scalars
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
-    const HeapRef<false> top{topk, topi, a.ef + 1, topk, topi};
+    const HeapRef<true> top{topk, topi, a.top_lds, a.top_ovf_k + (size_t)blockIdx.x * (size_t)a.top_ovf_cap,
+                            a.top_ovf_i + (size_t)blockIdx.x * (size_t)a.top_ovf_cap};
     const HeapRef<true> cand{cdk, cdi, a.cand_lds, a.cand_ovf_k + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap,
                        a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap};
     const int cand_cap = a.cand_lds + (int)a.cand_ovf_cap;
@@ -316,15 +317,15 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
         const bool staged = nres <= a.cand_lds;
         if (staged)
             for (int e = lane; e < nres; e += 64)
-                lab[e] = a.labels[topi[e]];
+                lab[e] = a.labels[top.id(e)];
         __syncthreads();
         for (int e = lane; e < nres; e += 64) {
-            const float de = topk[e];
-            const uint64_t le = staged ? lab[e] : a.labels[topi[e]];
+            const float de = top.key(e);
+            const uint64_t le = staged ? lab[e] : a.labels[top.id(e)];
             int rank = 0;
             for (int o = 0; o < nres; ++o) {
-                const float dq = topk[o];
-                const uint64_t lo = staged ? lab[o] : a.labels[topi[o]];
+                const float dq = top.key(o);
+                const uint64_t lo = staged ? lab[o] : a.labels[top.id(o)];
                 rank += (dq < de) || (dq == de && lo < le);
             }
             Dq[rank] = de;
@@ -366,7 +367,9 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     int cus = 0;
     DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
     const int cand_lds = 512;
-    const size_t lds = sizeof(float) * (size_t)ix.d + 8 * (size_t)(efc + 1) + 8 * (size_t)cand_lds +
+    const int top_lds = std::min(efc + 1, 1024); // top_candidates beyond this continue in global memory
+    const int64_t top_ovf = (int64_t)efc + 1 - top_lds;
+    const size_t lds = sizeof(float) * (size_t)ix.d + 8 * (size_t)top_lds + 8 * (size_t)cand_lds +
                        8 * (size_t)ix.maxM0 + 16;
     if (lds > 160 * 1024)
         throw Error(DRM_ERR_UNSUPPORTED, "fp32 search workspace does not fit in LDS (ef too large)");
@@ -374,8 +377,9 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     const int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
     const int64_t words = (ix.ntotal + 31) / 32;
     const int64_t ovf_cap = 16384;
-    if (slots > ix.n_slots || words != ix.vis_words) {
-        for (void *p : {(void *)ix.visited, (void *)ix.clear_list, (void *)ix.cand_ovf_k, (void *)ix.cand_ovf_i})
+    if (slots > ix.n_slots || words != ix.vis_words || top_ovf > ix.top_ovf_cap) {
+        for (void *p : {(void *)ix.visited, (void *)ix.clear_list, (void *)ix.cand_ovf_k, (void *)ix.cand_ovf_i,
+                        (void *)ix.top_ovf_k, (void *)ix.top_ovf_i})
             if (p)
                 DRM_HIP_CHECK(hipFree(p));
         const int alloc = std::max(slots, cus * per_cu);
@@ -387,6 +391,9 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)alloc * (size_t)ix.clear_cap));
         DRM_HIP_CHECK(hipMalloc(&ix.cand_ovf_k, sizeof(float) * (size_t)alloc * (size_t)ovf_cap));
         DRM_HIP_CHECK(hipMalloc(&ix.cand_ovf_i, sizeof(uint32_t) * (size_t)alloc * (size_t)ovf_cap));
+        ix.top_ovf_cap = std::max<int64_t>(top_ovf, 1);
+        DRM_HIP_CHECK(hipMalloc(&ix.top_ovf_k, sizeof(float) * (size_t)alloc * (size_t)ix.top_ovf_cap));
+        DRM_HIP_CHECK(hipMalloc(&ix.top_ovf_i, sizeof(uint32_t) * (size_t)alloc * (size_t)ix.top_ovf_cap));
         ix.n_slots = alloc;
     }
     if (!ix.counter)
@@ -422,6 +429,10 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.cand_ovf_k = ix.cand_ovf_k;
     a.cand_ovf_i = ix.cand_ovf_i;
     a.cand_ovf_cap = ix.cand_ovf_cap;
+    a.top_lds = top_lds;
+    a.top_ovf_k = ix.top_ovf_k;
+    a.top_ovf_i = ix.top_ovf_i;
+    a.top_ovf_cap = ix.top_ovf_cap;
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 2 * sizeof(uint32_t), stream));
     hipLaunchKernelGGL(hnsw_flat_search_kernel, dim3(slots), dim3(64), lds, stream, a);
     DRM_HIP_CHECK(hipGetLastError());
