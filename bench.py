@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
 SEARCH_KERNEL = "hnsw_pq_search_kernel<2, true, 0, true, false>"  # what C3 (ef = k = 128, PQ8x8) launches
+FLAT_KERNEL = "hnsw_flat_search_kernel"  # --index flat
 SW_KERNEL = "sw_score_f16_kernel<152>"
 SW_VALU_PER_CELL = 556 / 152 / 2  # static ISA count of the sw_score_f16_kernel<152> row loop: 556 VALU per 152 cell pairs
 
@@ -110,20 +111,25 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn):
-    """Oracle (C restatement, OpenMP over queries) on a bounded sample of this workload."""
-    from oracle import faiss_file, oracle as O
+def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=False):
+    """Oracle (C / C++ restatement, OpenMP over queries) on a bounded sample of this workload."""
+    from oracle import faiss_file, hnswlib_file, oracle as O
     from deepreadmapper_amd.rerank import pack_queries
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
-    fx = faiss_file.read(index_path)
-    s = O.make_index(fx)
+    if flat:
+        fx = hnswlib_file.read(index_path)
+    else:
+        s = O.make_index(faiss_file.read(index_path))
     refs = w.refs
 
     def run(n):
         q = q_emb[:n]
         t0 = time.perf_counter()
-        D, I, nd, nh = O.hnswpq_search(s, q, k, ef, nthreads=threads)
+        if flat:
+            D, I, nd, nh = O.hnswlib_search(fx, q, k, ef, nthreads=threads)
+        else:
+            D, I, nd, nh = O.hnswpq_search(s, q, k, ef, nthreads=threads)
         t1 = time.perf_counter()
         qbuf, ql = queries[:n], np.full(n, queries.shape[1], dtype=np.int32)
         rc, sc, ids, cnt = O.post_process_sw_static(I, refs, refs.shape[1], qbuf, ql, 1, k, k, nthreads=threads)
@@ -272,6 +278,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--build-threads", type=int, default=0)
+    ap.add_argument("--index", choices=["pq", "flat"], default="pq",
+                    help="pq (default): faiss IndexHNSWPQ, the live pipeline's index; flat: hnswlib fp32-L2 "
+                         "index (M=64, EFC=128, the reference's hnswlib defaults) over the same windows")
     ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
                     help="c3 (default, the headline): search + SW rerank; c4: search only on a 10M-vector "
                          "sparse (stride 4) index, SURVEY.md sec. 8d")
@@ -306,7 +315,21 @@ def main():
     queries = np.ascontiguousarray(w.queries[lo:hi])
     truth = w.truth[lo:hi]
 
-    ix = HnswPqIndex(w.index_path, dev)
+    flat = args.index == "flat"
+    if flat:
+        from deepreadmapper_amd.flat import HnswFlatIndex
+        fpath = os.path.join(args.cache, "c3_flat_M64_efc128.hnsw")
+        if D.rank == 0 and not os.path.exists(fpath):
+            t0 = time.time()
+            synth.build_flat_index(synth.embed(synth.tag(w.refs)), fpath + ".tmp", M=64, efc=128,
+                                   nthreads=args.build_threads)
+            os.replace(fpath + ".tmp", fpath)
+            log(f"[bench] hnswlib fp32 index built in {time.time() - t0:.1f}s")
+        D.barrier()
+        ix = HnswFlatIndex(fpath, dev)
+        d_L = DeviceBuffer((Q, K), np.uint64)
+    else:
+        ix = HnswPqIndex(w.index_path, dev)
     table = WindowTable(w.refs, dev)
     d_x = DeviceBuffer.from_host(q_emb)
     d_q = DeviceBuffer.from_host(queries)
@@ -320,10 +343,14 @@ def main():
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        ix.search_device(d_x, Q, K, EF, d_D, d_I, d_nd, d_nh, stream, d_nhops_upper=d_nu)
+        if flat:
+            ix.search_device(d_x, Q, K, EF, d_D, d_L, d_nd, d_nh, stream, d_nhops_upper=d_nu)
+        else:
+            ix.search_device(d_x, Q, K, EF, d_D, d_I, d_nd, d_nh, stream, d_nhops_upper=d_nu)
         if ev:
             ev[1].record(stream)
-        check(lib().drm_post_process_sw_static_device(table.handle, d_I.ptr, Q, K, d_q.ptr, d_ql.ptr,
+        check(lib().drm_post_process_sw_static_device(table.handle, (d_L if flat else d_I).ptr, Q, K, d_q.ptr,
+                                                      d_ql.ptr,
                                                       queries.shape[1], 1, K, K, d_sc.ptr, d_id.ptr, d_st.ptr,
                                                       stream.handle))
         if ev:
@@ -347,7 +374,9 @@ def main():
     sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
 
     # correctness / quality of this rank's last step
-    n_fallback = ix.fallbacks()
+    n_fallback = ix.overflows() if flat else ix.fallbacks()
+    if flat and n_fallback:
+        raise SystemExit(f"{n_fallback} queries outgrew the GPU candidate heap")
     st = d_st.download()
     if not (st == K).all():
         raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")
@@ -359,15 +388,21 @@ def main():
     # algorithmic bytes of the search kernel, per launch:
     #   512 (query) + 2*M*4 per level-0 hop + M*4 per upper hop + ndis*code_size + K*12 (ids+dists)
     info = ix.info
-    deg0 = 2 * info.M_hnsw
-    code = (info.pq_M * info.pq_nbits + 7) // 8
     l0 = nhops - nup
-    bytes_q = 4 * info.d + l0 * deg0 * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
-    codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
-    bytes_launch = float(bytes_q.sum() + codebook)
+    if flat:
+        # fp32: a level-0 row is maxM0 links + count, an upper row maxM + count, a distance a 4d-byte vector
+        bytes_q = 4 * info.d + l0 * (info.maxM0 + 1) * 4 + nup * (info.maxM + 1) * 4 + ndis * 4 * info.d + K * 12
+        bytes_launch = float(bytes_q.sum())
+    else:
+        deg0 = 2 * info.M_hnsw
+        code = (info.pq_M * info.pq_nbits + 7) // 8
+        bytes_q = 4 * info.d + l0 * deg0 * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
+        codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
+        bytes_launch = float(bytes_q.sum() + codebook)
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
     cells = float(Q) * K * w.refs.shape[1] * queries.shape[1]
-    prof_path, pmc = committed_pmc(SEARCH_KERNEL)
+    search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
+    prof_path, pmc = committed_pmc(search_kernel)
     traffic = None
     if pmc and "hbm_bytes_est" in pmc:
         traffic = float(pmc["hbm_bytes_est"])
@@ -379,24 +414,28 @@ def main():
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
-    gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_I),
+    gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_L if flat else d_I),
                                            ("search_dists", d_D)], {"sw_ids": ids})
     result = None
     if D.rank == 0:
         cpu = None
         if N == 1 and not args.no_cpu:
-            cpu = cpu_baseline(w, w.index_path, queries, q_emb, K, EF, args.cpu_budget, log)
+            cpu = cpu_baseline(w, fpath if flat else w.index_path, queries, q_emb, K, EF, args.cpu_budget, log,
+                               flat=flat)
+        workload = ("C3: synthetic 1M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200), search + SW "
+                    "rerank, EF=128 K=128") if not flat else (
+                    "C3-flat: the same 1M windows in an hnswlib fp32-L2 index (M=64, EFC=128), hnswlib searchKnn + "
+                    "SW rerank, EF=128 K=128")
         result = {
             "metric": "mapped reads/sec, 150 bp queries, EF=128 K=128",
             "value": round(value, 1), "unit": "reads/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32 (PQ-ADC distances) + int32 (SW DP)",
+            "vs_baseline": None,
+            "dtype": ("fp32 (L2 distances)" if flat else "fp32 (PQ-ADC distances)") + " + int32 (SW DP)",
             "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
-            "config": {"workload": "C3: synthetic 1M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 "
-                                   "EFC=200), search + SW rerank, EF=128 K=128",
-                       "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
+            "config": {"workload": workload, "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
-            "roofline": {"bound": "hbm", "kernel": SEARCH_KERNEL, "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": search_kernel, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": bytes_launch,
                          "avg_launch_ms": round(search_ms, 4),

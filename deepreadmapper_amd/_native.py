@@ -109,7 +109,7 @@ def lib():
         "drm_flat_index_free": (C.c_int, [vp]),
         "drm_flat_index_get_info": (C.c_int, [vp, C.POINTER(FlatIndexInfo)]),
         "drm_flat_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
-        "drm_flat_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
+        "drm_flat_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),
         "drm_flat_search_overflows": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_build_hnsw_flat": (C.c_int, [vp, i64, i32, i32, i32, i32, C.c_uint64, C.c_char_p]),
         "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),

@@ -497,7 +497,8 @@ int drm_flat_index_get_info(const drm_flat_index *index, drm_flat_index_info *in
 }
 
 int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
-                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, void *stream)
+                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper,
+                           void *stream)
 {
     return guarded([&] {
         if (!index || (n > 0 && (!d_x || !d_D || !d_labels || !d_ndis || !d_nhops)))
@@ -505,7 +506,7 @@ int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, i
         if (n <= 0)
             throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswlib_dir/search.cpp:20-23
         DRM_HIP_CHECK(hipSetDevice(index->dev.device));
-        drm::launch_hnsw_flat_search(index->dev, d_x, n, k, ef, d_D, d_labels, d_ndis, d_nhops,
+        drm::launch_hnsw_flat_search(index->dev, d_x, n, k, ef, d_D, d_labels, d_ndis, d_nhops, d_nhops_upper,
                                      (hipStream_t)stream);
     });
 }
@@ -546,7 +547,7 @@ int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d,
         DRM_HIP_CHECK(hipEventCreate(&e0));
         DRM_HIP_CHECK(hipEventCreate(&e1));
         DRM_HIP_CHECK(hipEventRecord(e0, nullptr));
-        drm::launch_hnsw_flat_search(index->dev, dx.p, n, k, ef, dD.p, dL.p, dst.p, dst.p + n, nullptr);
+        drm::launch_hnsw_flat_search(index->dev, dx.p, n, k, ef, dD.p, dL.p, dst.p, dst.p + n, nullptr, nullptr);
         DRM_HIP_CHECK(hipEventRecord(e1, nullptr));
         DRM_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0.f;

@@ -140,6 +140,7 @@ struct FlatArgs {
     float *D;
     uint64_t *L;
     int32_t *ndis, *nhops;
+    int32_t *nhops_upper; // optional: greedy hops on levels >= 1 (for the bytes model)
     uint32_t *visited;
     int64_t vis_words;
     int32_t *clear_list;
@@ -157,7 +158,8 @@ struct FlatArgs {
 };
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,
-                             uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream);
+                             uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper,
+                             hipStream_t stream);
 
 // ---------------------------------------------------------------------------------- SW rerank
 struct DeviceRefs {

@@ -169,6 +169,8 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
             if (lane == 0) {
                 a.ndis[qi] = 0;
                 a.nhops[qi] = 0;
+                if (a.nhops_upper)
+                    a.nhops_upper[qi] = 0;
             }
             continue;
         }
@@ -184,6 +186,7 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
         l2_items(a, q, fid, 1, fd);
         float curdist = fd[0];
         ndis++;
+        int nhops_up = 0;
         for (int level = a.maxlevel; level > 0; --level) {
             for (;;) {
                 const uint32_t *blk = a.up + a.up_off[cur] + (int64_t)(level - 1) * (1 + a.maxM);
@@ -192,6 +195,7 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
                     fid[j] = blk[1 + j];
                 __syncthreads();
                 nhops++;
+                nhops_up++;
                 ndis += size;
                 l2_items(a, q, fid, size, fd);
                 bool changed = false;
@@ -338,6 +342,8 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
         if (lane == 0) {
             a.ndis[qi] = ndis;
             a.nhops[qi] = nhops;
+            if (a.nhops_upper)
+                a.nhops_upper[qi] = nhops_up;
         }
         // VisitedTable reset: clear exactly the bits this query set
         if (clear_n <= a.clear_cap) {
@@ -355,7 +361,8 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
 } // namespace
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,
-                             uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, hipStream_t stream)
+                             uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper,
+                             hipStream_t stream)
 {
     if (n <= 0)
         return;
@@ -419,6 +426,7 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.L = d_L;
     a.ndis = d_ndis;
     a.nhops = d_nhops;
+    a.nhops_upper = d_nhops_upper;
     a.visited = ix.visited;
     a.vis_words = ix.vis_words;
     a.clear_list = ix.clear_list;

@@ -44,10 +44,12 @@ class HnswFlatIndex:
         check(lib().drm_flat_search(self.handle, ptr(x), n, d, int(k), int(ef), ptr(D), ptr(L), C.byref(st)))
         return D, L, st
 
-    def search_device(self, d_x, n, k, ef, d_D, d_L, d_ndis, d_nhops, stream=None):
+    def search_device(self, d_x, n, k, ef, d_D, d_L, d_ndis, d_nhops, stream=None, d_nhops_upper=None):
         """Search on device buffers (DeviceBuffer), enqueued on `stream`."""
         check(lib().drm_flat_search_device(self.handle, d_x.ptr, int(n), int(k), int(ef), d_D.ptr, d_L.ptr,
-                                           d_ndis.ptr, d_nhops.ptr, stream.handle if stream is not None else None))
+                                           d_ndis.ptr, d_nhops.ptr,
+                                           d_nhops_upper.ptr if d_nhops_upper is not None else None,
+                                           stream.handle if stream is not None else None))
 
     def overflows(self):
         c = C.c_int64(0)

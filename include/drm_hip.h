@@ -127,9 +127,11 @@ int drm_flat_index_get_info(const drm_flat_index *index, drm_flat_index_info *in
  * (+inf, 2^64-1). Throws "Query data is empty" (-1) for n == 0 (search.cpp:20-23). */
 int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d, int32_t k, int32_t ef, float *D,
                     uint64_t *labels, drm_search_stats *stats);
-/* Same on device buffers, enqueued on `stream`; d_ndis/d_nhops [n] receive per-query counts. */
+/* Same on device buffers, enqueued on `stream`; d_ndis/d_nhops [n] receive per-query counts,
+ * d_nhops_upper [n] (may be NULL) the hops on levels >= 1 contained in nhops. */
 int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
-                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, void *stream);
+                           uint64_t *d_labels, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper,
+                           void *stream);
 /* Diagnostic: queries of the last search whose candidate_set outgrew the GPU heap (their outputs
  * are invalid; drm_flat_search reports it as an error). Synchronizes the device. */
 int drm_flat_search_overflows(drm_flat_index *index, int64_t *count);
