@@ -398,8 +398,8 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
 namespace {
 void free_flat(drm::DeviceFlatIndex &d)
 {
-    void *ptrs[] = {d.vec,     d.l0,         d.l0cnt,      d.up_off,     d.up,        d.labels,   d.visited,
-                    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter};
+    void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,    d.up,        d.labels,  d.visited,
+                    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -451,6 +451,11 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
         }
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
+            if (std::atoi(e)) {
+                DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
+                DRM_HIP_CHECK(hipMemset(d.stamps, 0, 8 * sizeof(uint64_t)));
+            }
         d.vec = upload_vec(h.vec, d.device_bytes);
         d.l0 = upload_vec(l0, d.device_bytes);
         d.l0cnt = upload_vec(cnt, d.device_bytes);
@@ -508,6 +513,16 @@ int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, i
         DRM_HIP_CHECK(hipSetDevice(index->dev.device));
         drm::launch_hnsw_flat_search(index->dev, d_x, n, k, ef, d_D, d_labels, d_ndis, d_nhops, d_nhops_upper,
                                      (hipStream_t)stream);
+    });
+}
+
+int drm_debug_flat_stamps(drm_flat_index *index, uint64_t *out8)
+{
+    return guarded([&] {
+        if (!index || !index->dev.stamps)
+            throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
+        DRM_HIP_CHECK(hipMemcpy(out8, index->dev.stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 8 * sizeof(uint64_t)));
     });
 }
 

@@ -118,6 +118,7 @@ struct DeviceFlatIndex {
     float *top_ovf_k = nullptr;
     uint32_t *top_ovf_i = nullptr;
     uint32_t *counter = nullptr;    // [0] work queue head, [1] candidate_set overflows
+    uint64_t *stamps = nullptr;     // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     int64_t device_bytes = 0;
     HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
 };
@@ -155,6 +156,7 @@ struct FlatArgs {
     float *top_ovf_k;
     uint32_t *top_ovf_i;
     int64_t top_ovf_cap;
+    uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1)
 };
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,

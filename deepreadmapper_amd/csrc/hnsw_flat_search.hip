@@ -96,6 +96,113 @@ template <bool OVF> __device__ void stl_pop(const HeapRef<OVF> &h, int len)
     h.set(hole, vk, vi);
 }
 
+// ---- wave-parallel versions of the same two heap operations, for a heap held entirely in LDS.
+// They leave exactly the layout the serial replay above leaves (so every later tie resolves the same
+// way), but cost one LDS round trip plus a few ballots instead of one dependent LDS access per level.
+__device__ __forceinline__ int heap_depth(int slot) { return 31 - __builtin_clz((unsigned)slot + 1u); }
+
+// __push_heap for the element just appended at slot len-1. Along the ancestor chain keys only grow
+// (parent >= child), so the ancestors that move down are exactly those with key < vk: lane j reads
+// ancestor j+1, one ballot counts them (h), they shift down one level and vk lands at ancestor h.
+// Returns true when vk became the root.
+__device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float vk, uint32_t vi)
+{
+    const int lane = lane_id();
+    const int hole = len - 1;
+    const int m = heap_depth(hole);
+    const int j = lane + 1;
+    const bool valid = j <= m;
+    const int anc = valid ? ((hole + 1) >> j) - 1 : 0;
+    const float ak = K[anc];
+    const uint32_t ai = I[anc];
+    const bool lt = valid && ak < vk;
+    const int h = __popcll(__ballot(lt));
+    if (lt) { // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
+        const int dst = ((hole + 1) >> (j - 1)) - 1;
+        K[dst] = ak;
+        I[dst] = ai;
+    }
+    if (lane == 0) {
+        const int dst = ((hole + 1) >> h) - 1;
+        K[dst] = vk;
+        I[dst] = vi;
+    }
+    return h == m;
+}
+
+// pop_heap + pop_back for len > 1 (libstdc++ __adjust_heap then __push_heap of the old last
+// element): the hole walks from the root to a leaf along the larger child (ties -> right child, a
+// lone left child taken), then the old last element v sifts back up that same path. Net effect on
+// the path P_0 = root .. P_m = leaf: with h = #{i >= 1 : key(P_i) < v}, P_0 .. P_{m-h-1} each take
+// their successor's entry, P_{m-h} takes v, the rest stay. Lanes own nodes p = lane + 64 jj and hold
+// both children of p, so the child choices are one ballot per 64 nodes; the leaf is found by a scalar
+// walk over those bits. NN = node groups (L <= 128 NN + 1). Returns the new root key.
+template <int NN> __device__ __forceinline__ float par_pop(float *K, uint32_t *I, int len)
+{
+    const int lane = lane_id();
+    const int L = len - 1;
+    const float vk = K[L];
+    const uint32_t vi = I[L];
+    float ck[NN];
+    uint32_t ci[NN];
+    uint64_t bits[NN];
+#pragma unroll
+    for (int jj = 0; jj < NN; ++jj) {
+        const int p = lane + 64 * jj;
+        const bool has_l = 2 * p + 1 < L, has_r = 2 * p + 2 < L;
+        const float lk = K[has_l ? 2 * p + 1 : 0], rk = K[has_r ? 2 * p + 2 : 0];
+        const uint32_t li = I[has_l ? 2 * p + 1 : 0], ri = I[has_r ? 2 * p + 2 : 0];
+        const bool right = has_r && !(rk < lk);
+        ck[jj] = right ? rk : lk;
+        ci[jj] = right ? ri : li;
+        bits[jj] = __ballot(right);
+    }
+    int leaf = 0;
+    while (2 * leaf + 1 < L) {
+        uint64_t mk = bits[0];
+#pragma unroll
+        for (int jj = 1; jj < NN; ++jj)
+            if ((leaf >> 6) == jj)
+                mk = bits[jj];
+        leaf = 2 * leaf + 1 + (int)((mk >> (leaf & 63)) & 1ull);
+    }
+    const int m = heap_depth(leaf);
+    int h = 0;
+    bool on[NN];
+#pragma unroll
+    for (int jj = 0; jj < NN; ++jj) {
+        const int p = lane + 64 * jj;
+        const int dp = heap_depth(p);
+        on[jj] = dp < m && (((leaf + 1) >> (m - dp)) == p + 1);
+        h += __popcll(__ballot(on[jj] && ck[jj] < vk));
+    }
+    const int t = m - h; // depth where v lands
+#pragma unroll
+    for (int jj = 0; jj < NN; ++jj) {
+        const int p = lane + 64 * jj;
+        if (on[jj] && heap_depth(p) < t) {
+            K[p] = ck[jj];
+            I[p] = ci[jj];
+        }
+    }
+    if (lane == 0) {
+        const int dst = ((leaf + 1) >> h) - 1;
+        K[dst] = vk;
+        I[dst] = vi;
+    }
+    return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ck[0]), 0)) : vk;
+}
+
+__device__ __forceinline__ float par_pop_any(float *K, uint32_t *I, int len)
+{
+    const int L = len - 1;
+    if (L <= 128)
+        return par_pop<1>(K, I, len);
+    if (L <= 512)
+        return par_pop<4>(K, I, len);
+    return par_pop<8>(K, I, len);
+}
+
 __device__ __forceinline__ uint32_t dpp_row_shr1(uint32_t v)
 {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
@@ -132,10 +239,92 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
     __syncthreads();
 }
 
+// Same distances with the query slice in registers (qr[r] = q[sub + 8r], NV = d / 8 per lane) and
+// every load of a pass issued before the first use: 16 items per pass, two per lane group, so a
+// hop's distances cost one memory round trip instead of one per dimension step.
+template <int NV>
+__device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float (&qr)[NV], const uint32_t *ids,
+                                             int nitem, float *out)
+{
+    const int lane = lane_id(), grp = lane >> 3, sub = lane & 7;
+    for (int base = 0; base < nitem; base += 16) {
+        const int f0 = base + grp, f1 = base + 8 + grp;
+        const bool two = base + 8 < nitem; // wave-uniform
+        const float *v0 = a.vec + (size_t)ids[min(f0, nitem - 1)] * (size_t)(8 * NV) + sub;
+        const float *v1 = a.vec + (size_t)ids[min(f1, nitem - 1)] * (size_t)(8 * NV) + sub;
+        float t0[NV], t1[NV];
+#pragma unroll
+        for (int r = 0; r < NV; ++r)
+            t0[r] = v0[8 * r];
+        if (two) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r)
+                t1[r] = v1[8 * r];
+        }
+        float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < NV; ++r) {
+            const float df = __fsub_rn(qr[r], t0[r]);
+            acc0 = __fadd_rn(acc0, __fmul_rn(df, df));
+        }
+        uint32_t p0 = __float_as_uint(acc0);
+#pragma unroll
+        for (int s = 1; s < 8; ++s) {
+            const uint32_t t = dpp_row_shr1(p0);
+            if (sub == s)
+                p0 = __float_as_uint(__fadd_rn(__uint_as_float(t), __uint_as_float(p0)));
+        }
+        if (f0 < nitem && sub == 7)
+            out[f0] = __uint_as_float(p0);
+        if (two) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r) {
+                const float df = __fsub_rn(qr[r], t1[r]);
+                acc1 = __fadd_rn(acc1, __fmul_rn(df, df));
+            }
+            uint32_t p1 = __float_as_uint(acc1);
+#pragma unroll
+            for (int s = 1; s < 8; ++s) {
+                const uint32_t t = dpp_row_shr1(p1);
+                if (sub == s)
+                    p1 = __float_as_uint(__fadd_rn(__uint_as_float(t), __uint_as_float(p1)));
+            }
+            if (f1 < nitem && sub == 7)
+                out[f1] = __uint_as_float(p1);
+        }
+    }
+    __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, const float (&qr)[NV > 0 ? NV : 1],
+                                            const uint32_t *ids, int nitem, float *out)
+{
+    if constexpr (NV > 0)
+        l2_items_reg<NV>(a, qr, ids, nitem, out);
+    else
+        l2_items(a, q, ids, nitem, out);
+}
+
+#define FLAT_STAMP(idx)                                                                                     \
+    do {                                                                                                    \
+        if (STAMPS) {                                                                                       \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                                               \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            st_acc[idx] += _t - st_last;                                                                    \
+            st_last = _t;                                                                                   \
+        }                                                                                                   \
+    } while (0)
+
+// NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path
+template <int NV, bool STAMPS>
 __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     float *q = reinterpret_cast<float *>(smem);                      // [d]
     float *topk = q + a.d;                                           // [top_lds]
     uint32_t *topi = reinterpret_cast<uint32_t *>(topk + a.top_lds); // [top_lds]
@@ -174,8 +363,15 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
             }
             continue;
         }
-        for (int t = lane; t < a.d; t += 64)
-            q[t] = a.x[(int64_t)qi * a.d + t];
+        float qr[NV > 0 ? NV : 1];
+        if constexpr (NV > 0) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r)
+                qr[r] = a.x[(int64_t)qi * a.d + (lane & 7) + 8 * r];
+        } else {
+            for (int t = lane; t < a.d; t += 64)
+                q[t] = a.x[(int64_t)qi * a.d + t];
+        }
         __syncthreads();
         int ndis = 0, nhops = 0;
         // --- searchKnn: greedy descent on levels maxlevel .. 1
@@ -183,7 +379,7 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
         if (lane == 0)
             fid[0] = cur;
         __syncthreads();
-        l2_items(a, q, fid, 1, fd);
+        l2_dispatch<NV>(a, q, qr, fid, 1, fd);
         float curdist = fd[0];
         ndis++;
         int nhops_up = 0;
@@ -197,7 +393,7 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
                 nhops++;
                 nhops_up++;
                 ndis += size;
-                l2_items(a, q, fid, size, fd);
+                l2_dispatch<NV>(a, q, qr, fid, size, fd);
                 bool changed = false;
                 for (int j = 0; j < size; ++j) { // sequential `if (d < curdist)` (uniform)
                     const float dd = fd[j];
@@ -224,97 +420,194 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
                 clr[0] = (int32_t)cur;
         }
         __syncthreads();
+        FLAT_STAMP(0); // query setup + upper levels
+        // row of the predicted next candidate, loaded while lane 0 works the heaps (maxM0 <= 128)
+        uint32_t pf_c = ~0u, pf_w0 = 0u, pf_w1 = 0u;
+        int pf_cnt = 0;
+        const bool narrow = a.maxM0 <= 128;
+        const bool top_par = a.ef + 1 <= a.top_lds; // top_candidates entirely in LDS
         while (cand_len > 0) {
             const float cdist = -cand.key(0);
             if (cdist > lowerBound)
                 break;
             const uint32_t c = cand.id(0);
             __syncthreads();
-            if (lane == 0)
-                stl_pop(cand, cand_len);
+            if (cand_len > 1) {
+                if (cand_len <= a.cand_lds) {
+                    par_pop_any(cdk, cdi, cand_len);
+                } else {
+                    if (lane == 0)
+                        stl_pop(cand, cand_len);
+                    __syncthreads();
+                }
+            }
             cand_len--;
             nhops++;
+            FLAT_STAMP(1); // candidate_set pop
             // the row of c: maxM0 links, lane j holds links j, j + 64, ...
-            const int cnt = (int)(a.l0cnt[c] & 0xFFFFu);
             const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
+            int cnt;
+            uint32_t r0, r1;
+            if (c == pf_c) {
+                cnt = pf_cnt;
+                r0 = pf_w0;
+                r1 = pf_w1;
+            } else {
+                cnt = (int)(a.l0cnt[c] & 0xFFFFu);
+                r0 = row[min(lane, a.maxM0 - 1)];
+                r1 = row[min(64 + lane, a.maxM0 - 1)];
+            }
+            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
             int nf = 0;
-            for (int base = 0; base < cnt; base += 64) {
-                const int j = base + lane;
-                const bool act = j < cnt;
-                const uint32_t v = act ? row[j] : 0u;
-                bool fresh = false;
-                if (act) {
-                    const uint32_t bit = 1u << (v & 31);
-                    fresh = (atomicOr(&vis[v >> 5], bit) & bit) == 0u;
-                }
+            for (int base = 0; base < cnt; base += 128) { // one pass when maxM0 <= 128
+                const int j0 = base + lane, j1 = base + 64 + lane;
+                const bool act0 = j0 < cnt, act1 = j1 < cnt;
+                const uint32_t v0 = base == 0 ? r0 : row[min(j0, a.maxM0 - 1)];
+                const uint32_t v1 = base == 0 ? r1 : row[min(j1, a.maxM0 - 1)];
+                const uint32_t b0 = 1u << (v0 & 31), b1 = 1u << (v1 & 31);
+                uint32_t o0 = ~0u, o1 = ~0u;
+                if (act0)
+                    o0 = atomicOr(&vis[v0 >> 5], b0);
+                if (act1)
+                    o1 = atomicOr(&vis[v1 >> 5], b1);
+                bool fresh0 = (o0 & b0) == 0u, fresh1 = (o1 & b1) == 0u;
                 if (a.check_dups) { // a repeated link in one row: only its first occurrence is fresh
                     for (int jj = 0; jj < cnt; ++jj) {
                         const uint32_t vj = row[jj];
-                        if (jj < j && vj == v)
-                            fresh = false;
+                        fresh0 = fresh0 && !(jj < j0 && vj == v0);
+                        fresh1 = fresh1 && !(jj < j1 && vj == v1);
                     }
                 }
-                const uint64_t fm = __ballot(fresh);
-                if (fresh) {
-                    const int p = nf + __popcll(fm & (lane ? (~0ull >> (64 - lane)) : 0ull));
-                    fid[p] = v;
+                const uint64_t fm0 = __ballot(fresh0), fm1 = __ballot(fresh1);
+                const int n0 = __popcll(fm0);
+                if (fresh0) {
+                    const int p = nf + __popcll(fm0 & below);
+                    fid[p] = v0;
                     if (clear_n + p < a.clear_cap)
-                        clr[clear_n + p] = (int32_t)v;
+                        clr[clear_n + p] = (int32_t)v0;
                 }
-                nf += __popcll(fm);
+                if (fresh1) {
+                    const int p = nf + n0 + __popcll(fm1 & below);
+                    fid[p] = v1;
+                    if (clear_n + p < a.clear_cap)
+                        clr[clear_n + p] = (int32_t)v1;
+                }
+                nf += n0 + __popcll(fm1);
             }
             clear_n += nf;
             __syncthreads();
-            l2_items(a, q, fid, nf, fd);
+            FLAT_STAMP(2); // row + visited
+            l2_dispatch<NV>(a, q, qr, fid, nf, fd);
             ndis += nf;
-            // sequential consideration in link order (lane 0 owns both heaps)
-            if (lane == 0) {
-                int tl = top_len, cl = cand_len;
-                float lb = lowerBound;
-                for (int f = 0; f < nf; ++f) {
-                    const float dist = fd[f];
-                    if (tl < a.ef || lb > dist) {
-                        if (cl >= cand_cap) {
-                            overflow = true;
-                            break;
-                        }
-                        cand.set(cl, -dist, fid[f]);
-                        stl_push(cand, ++cl, -dist, fid[f]);
-                        top.set(tl, dist, fid[f]);
-                        stl_push(top, ++tl, dist, fid[f]);
-                        while (tl > a.ef) {
-                            stl_pop(top, tl);
-                            tl--;
-                        }
-                        lb = top.key(0);
+            FLAT_STAMP(3); // distances
+            if (narrow) {
+                // next pop = the nearer of the candidate_set root and the nearest fresh item that
+                // passes the current bound; issue its row loads now, consume them next hop
+                float bd = INFINITY;
+                int bf = 0x7FFFFFFF;
+                for (int f = lane; f < nf; f += 64) {
+                    const float d = fd[f];
+                    if (d < bd) {
+                        bd = d;
+                        bf = f;
                     }
                 }
-                sh[0] = tl;
-                sh[1] = cl;
-                sh[2] = __float_as_int(lb);
-                sh[3] = overflow ? 1 : 0;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) {
+                    const float od = __shfl_xor(bd, off);
+                    const int of = __shfl_xor(bf, off);
+                    if (od < bd || (od == bd && of < bf)) {
+                        bd = od;
+                        bf = of;
+                    }
+                }
+                const float croot = cand_len > 0 ? -cand.key(0) : INFINITY;
+                uint32_t pred = ~0u;
+                if (bf < nf && (top_len < a.ef || bd < lowerBound) && bd < croot)
+                    pred = fid[bf];
+                else if (cand_len > 0)
+                    pred = cand.id(0);
+                pred = __builtin_amdgcn_readfirstlane(pred);
+                if (pred != ~0u && pred != pf_c) {
+                    const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
+                    pf_c = pred;
+                    pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
+                    pf_w0 = prow[min(lane, a.maxM0 - 1)];
+                    pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
+                }
+            }
+            // consideration in link order: `if (top.size() < ef || lowerBound > dist)` push both heaps,
+            // trim top to ef. lowerBound only falls once top is full, so one ballot per 64 links
+            // picks a superset of the accepted ones and only those are visited (exact test rechecked).
+            for (int base = 0; base < nf; base += 64) {
+                const int f = base + lane;
+                const float dl = f < nf ? fd[f] : INFINITY;
+                const uint32_t il = f < nf ? fid[f] : 0u;
+                uint64_t mask = __ballot(f < nf && (top_len < a.ef || lowerBound > dl));
+                while (mask) {
+                    const int b = __builtin_ctzll(mask);
+                    mask &= mask - 1;
+                    const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
+                    if (!(top_len < a.ef || lowerBound > dist))
+                        continue;
+                    if (cand_len >= cand_cap) {
+                        overflow = true;
+                        break;
+                    }
+                    const uint32_t id = __builtin_amdgcn_readlane(il, b);
+                    if (++cand_len <= a.cand_lds) {
+                        par_push(cdk, cdi, cand_len, -dist, id);
+                    } else {
+                        if (lane == 0) {
+                            cand.set(cand_len - 1, -dist, id);
+                            stl_push(cand, cand_len, -dist, id);
+                        }
+                        __syncthreads();
+                    }
+                    ++top_len;
+                    if (top_par) {
+                        if (par_push(topk, topi, top_len, dist, id))
+                            lowerBound = dist;
+                        while (top_len > a.ef)
+                            lowerBound = par_pop_any(topk, topi, top_len--);
+                    } else {
+                        if (lane == 0) {
+                            top.set(top_len - 1, dist, id);
+                            stl_push(top, top_len, dist, id);
+                            int tl = top_len;
+                            while (tl > a.ef)
+                                stl_pop(top, tl--);
+                            sh[2] = __float_as_int(top.key(0));
+                        }
+                        __syncthreads();
+                        top_len = min(top_len, a.ef);
+                        lowerBound = __int_as_float(sh[2]);
+                    }
+                }
+                if (overflow)
+                    break;
             }
             __syncthreads();
-            top_len = sh[0];
-            cand_len = sh[1];
-            lowerBound = __int_as_float(sh[2]);
-            if (sh[3])
+            FLAT_STAMP(4); // consideration: heap pushes / pops
+            if (overflow)
                 break;
-            __syncthreads();
         }
         if (lane == 0 && overflow)
             atomicAdd(a.counter + 1, 1u); // candidate_set overflow: reported by the host entry points
         // --- while (top.size() > k) top.pop(); then order survivors by (dist, label)
-        if (lane == 0) {
-            int tl = top_len;
-            while (tl > a.k) {
-                stl_pop(top, tl);
-                tl--;
+        if (top_par) {
+            while (top_len > a.k)
+                par_pop_any(topk, topi, top_len--);
+        } else {
+            if (lane == 0) {
+                int tl = top_len;
+                while (tl > a.k)
+                    stl_pop(top, tl--);
             }
-            sh[0] = tl;
+            top_len = min(top_len, a.k);
         }
         __syncthreads();
-        const int nres = sh[0];
+        const int nres = top_len;
         // searchKnnCloserFirst order: ascending (dist, label) -- rank by counting, labels staged in
         // the (now idle) candidate-heap LDS when they fit
         uint64_t *lab = reinterpret_cast<uint64_t *>(cdk);
@@ -355,7 +648,11 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        FLAT_STAMP(5); // result ordering + reset
     }
+    if (STAMPS && lane == 0 && a.stamps)
+        for (int i = 0; i < 8; ++i)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
 } // namespace
@@ -442,7 +739,18 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.top_ovf_i = ix.top_ovf_i;
     a.top_ovf_cap = ix.top_ovf_cap;
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 2 * sizeof(uint32_t), stream));
-    hipLaunchKernelGGL(hnsw_flat_search_kernel, dim3(slots), dim3(64), lds, stream, a);
+    a.stamps = ix.stamps;
+    if (ix.d == 128) {
+        if (ix.stamps)
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, true>), dim3(slots), dim3(64), lds, stream, a);
+        else
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, false>), dim3(slots), dim3(64), lds, stream, a);
+    } else {
+        if (ix.stamps)
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, true>), dim3(slots), dim3(64), lds, stream, a);
+        else
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, false>), dim3(slots), dim3(64), lds, stream, a);
+    }
     DRM_HIP_CHECK(hipGetLastError());
 }
 
