@@ -374,9 +374,9 @@ def main():
     sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
 
     # correctness / quality of this rank's last step
-    n_fallback = ix.overflows() if flat else ix.fallbacks()
-    if flat and n_fallback:
-        raise SystemExit(f"{n_fallback} queries outgrew the GPU candidate heap")
+    if flat and ix.overflows():
+        raise SystemExit(f"{ix.overflows()} queries outgrew the GPU candidate heap")
+    n_fallback = ix.fallbacks()
     st = d_st.download()
     if not (st == K).all():
         raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")

@@ -29,7 +29,7 @@ EXPORTS = [
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
     "drm_build_hnswpq", "drm_build_hnsw_flat", "drm_embed_kmer3",
     "drm_flat_index_load", "drm_flat_index_free", "drm_flat_index_get_info", "drm_flat_search",
-    "drm_flat_search_device", "drm_flat_search_overflows",
+    "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_fallbacks",
 ]
 
 
@@ -111,6 +111,7 @@ def lib():
         "drm_flat_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_flat_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),
         "drm_flat_search_overflows": (C.c_int, [vp, C.POINTER(i64)]),
+        "drm_flat_search_fallbacks": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_build_hnsw_flat": (C.c_int, [vp, i64, i32, i32, i32, i32, C.c_uint64, C.c_char_p]),
         "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),
     }

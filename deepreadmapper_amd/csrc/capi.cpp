@@ -399,7 +399,8 @@ namespace {
 void free_flat(drm::DeviceFlatIndex &d)
 {
     void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,    d.up,        d.labels,  d.visited,
-                    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps};
+                    d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps,
+                    d.fb_list};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -451,6 +452,8 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
         }
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
+            d.try_sorted = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
             if (std::atoi(e)) {
                 DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
@@ -537,6 +540,20 @@ int drm_flat_search_overflows(drm_flat_index *index, int64_t *count)
             DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
         }
         *count = (int64_t)c[1];
+    });
+}
+
+int drm_flat_search_fallbacks(drm_flat_index *index, int64_t *count)
+{
+    return guarded([&] {
+        if (!index || !count)
+            throw Error(DRM_ERR_ARG, "null argument");
+        uint32_t c[3] = {0, 0, 0};
+        if (index->dev.counter) {
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+        }
+        *count = (int64_t)c[2];
     });
 }
 

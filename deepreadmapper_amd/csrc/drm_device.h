@@ -99,6 +99,7 @@ struct DeviceFlatIndex {
     int64_t ntotal = 0;
     int32_t has_dup_links = 0;
     int32_t waves_per_cu = 20;
+    int32_t try_sorted = 0;    // DRM_SEARCH_SORTED=1: tie-free sorted-array pass first, exact pass after
     float *vec = nullptr;      // [ntotal][d] f32 (512-B rows at d = 128)
     uint32_t *l0 = nullptr;    // [ntotal][maxM0] level-0 links (512-B rows at maxM0 = 128)
     uint32_t *l0cnt = nullptr; // [ntotal] link counts
@@ -117,7 +118,10 @@ struct DeviceFlatIndex {
     int64_t top_ovf_cap = 0;        // top_candidates entries beyond the LDS part (large ef), per slot
     float *top_ovf_k = nullptr;
     uint32_t *top_ovf_i = nullptr;
-    uint32_t *counter = nullptr;    // [0] work queue head, [1] candidate_set overflows
+    uint32_t *counter = nullptr;    // [0] queue head, [1] candidate_set overflows, [2] handed-over
+                                    // queries, [3] queue head of the exact pass
+    int32_t *fb_list = nullptr;     // queries the tie-free pass handed to the exact pass
+    int64_t fb_cap = 0;
     uint64_t *stamps = nullptr;     // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     int64_t device_bytes = 0;
     HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
@@ -156,7 +160,11 @@ struct FlatArgs {
     float *top_ovf_k;
     uint32_t *top_ovf_i;
     int64_t top_ovf_cap;
-    uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1)
+    uint64_t *stamps;     // diagnostic section timers (DRM_SEARCH_STAMPS=1)
+    const int32_t *qlist; // exact pass after the tie-free one: qlist[0 .. *qcount) instead of 0 .. n
+    const uint32_t *qcount;
+    int32_t *fb_list;     // tie-free pass: queries that met a distance tie
+    uint32_t *fb_count;
 };
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,

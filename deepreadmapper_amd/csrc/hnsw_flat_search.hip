@@ -193,14 +193,13 @@ template <int NN> __device__ __forceinline__ float par_pop(float *K, uint32_t *I
     return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ck[0]), 0)) : vk;
 }
 
+// heaps of up to 513 entries (the callers take the serial replay beyond)
 __device__ __forceinline__ float par_pop_any(float *K, uint32_t *I, int len)
 {
     const int L = len - 1;
     if (L <= 128)
         return par_pop<1>(K, I, len);
-    if (L <= 512)
-        return par_pop<4>(K, I, len);
-    return par_pop<8>(K, I, len);
+    return par_pop<4>(K, I, len);
 }
 
 __device__ __forceinline__ uint32_t dpp_row_shr1(uint32_t v)
@@ -306,6 +305,96 @@ __device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, c
         l2_items(a, q, ids, nitem, out);
 }
 
+// Links of c not yet visited, in row order -> fid[0 .. nf), each marked in the visited bitmap and
+// appended to the clear list. The row's first 128 words may already be in registers (prefetch).
+__device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_t *vis, int32_t *clr, int clear_n,
+                                          uint32_t *fid, bool have_pf, int pf_cnt, uint32_t pf_w0, uint32_t pf_w1)
+{
+    const int lane = lane_id();
+    const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
+    int cnt;
+    uint32_t r0, r1;
+    if (have_pf) {
+        cnt = pf_cnt;
+        r0 = pf_w0;
+        r1 = pf_w1;
+    } else {
+        cnt = (int)(a.l0cnt[c] & 0xFFFFu);
+        r0 = row[min(lane, a.maxM0 - 1)];
+        r1 = row[min(64 + lane, a.maxM0 - 1)];
+    }
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int nf = 0;
+    for (int base = 0; base < cnt; base += 128) { // one pass when maxM0 <= 128
+        const int j0 = base + lane, j1 = base + 64 + lane;
+        const bool act0 = j0 < cnt, act1 = j1 < cnt;
+        const uint32_t v0 = base == 0 ? r0 : row[min(j0, a.maxM0 - 1)];
+        const uint32_t v1 = base == 0 ? r1 : row[min(j1, a.maxM0 - 1)];
+        const uint32_t b0 = 1u << (v0 & 31), b1 = 1u << (v1 & 31);
+        uint32_t o0 = ~0u, o1 = ~0u;
+        if (act0)
+            o0 = atomicOr(&vis[v0 >> 5], b0);
+        if (act1)
+            o1 = atomicOr(&vis[v1 >> 5], b1);
+        bool fresh0 = (o0 & b0) == 0u, fresh1 = (o1 & b1) == 0u;
+        if (a.check_dups) { // a repeated link in one row: only its first occurrence is fresh
+            for (int jj = 0; jj < cnt; ++jj) {
+                const uint32_t vj = row[jj];
+                fresh0 = fresh0 && !(jj < j0 && vj == v0);
+                fresh1 = fresh1 && !(jj < j1 && vj == v1);
+            }
+        }
+        const uint64_t fm0 = __ballot(fresh0), fm1 = __ballot(fresh1);
+        const int n0 = __popcll(fm0);
+        if (fresh0) {
+            const int p = nf + __popcll(fm0 & below);
+            fid[p] = v0;
+            if (clear_n + p < a.clear_cap)
+                clr[clear_n + p] = (int32_t)v0;
+        }
+        if (fresh1) {
+            const int p = nf + n0 + __popcll(fm1 & below);
+            fid[p] = v1;
+            if (clear_n + p < a.clear_cap)
+                clr[clear_n + p] = (int32_t)v1;
+        }
+        nf += n0 + __popcll(fm1);
+    }
+    __syncthreads();
+    return nf;
+}
+
+// Nearest fresh item that passes the current bound (wave argmin over fd[0 .. nf)); +inf if none.
+__device__ __forceinline__ float nearest_fresh(const float *fd, int nf, int &bf)
+{
+    const int lane = lane_id();
+    float bd = INFINITY;
+    bf = 0x7FFFFFFF;
+    for (int f = lane; f < nf; f += 64) {
+        const float d = fd[f];
+        if (d < bd) {
+            bd = d;
+            bf = f;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float od = __shfl_xor(bd, off);
+        const int of = __shfl_xor(bf, off);
+        if (od < bd || (od == bd && of < bf)) {
+            bd = od;
+            bf = of;
+        }
+    }
+    bf = __builtin_amdgcn_readfirstlane(bf);
+    return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(bd)));
+}
+
+__device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false); // wave_shr:1
+}
+
 #define FLAT_STAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -317,8 +406,9 @@ __device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, c
         }                                                                                                   \
     } while (0)
 
-// NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path
-template <int NV, bool STAMPS>
+// NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
+// NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
+template <int NV, int NR, bool STAMPS>
 __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -338,16 +428,20 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
     const HeapRef<true> top{topk, topi, a.top_lds, a.top_ovf_k + (size_t)blockIdx.x * (size_t)a.top_ovf_cap,
                             a.top_ovf_i + (size_t)blockIdx.x * (size_t)a.top_ovf_cap};
     const HeapRef<true> cand{cdk, cdi, a.cand_lds, a.cand_ovf_k + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap,
-                       a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap};
+                             a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap};
     const int cand_cap = a.cand_lds + (int)a.cand_ovf_cap;
+    // queue: 0 .. n-1, or (fallback pass) the *qcount query ids in qlist
+    const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
 
     for (;;) {
         int qi = 0;
         if (lane == 0)
             qi = (int)atomicAdd(a.counter, 1u);
         qi = __builtin_amdgcn_readfirstlane(qi);
-        if ((int64_t)qi >= a.n)
+        if ((int64_t)qi >= nq)
             break;
+        if (a.qlist)
+            qi = __builtin_amdgcn_readfirstlane(a.qlist[qi]);
         float *Dq = a.D + (int64_t)qi * a.k;
         uint64_t *Lq = a.L + (int64_t)qi * a.k;
         if (a.ntotal == 0) {
@@ -409,234 +503,326 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
             }
         }
         // --- searchBaseLayerST<bare_bone_search = true>(cur, q, max(ef, k))
-        int top_len = 1, cand_len = 1, clear_n = 1;
-        float lowerBound = curdist;
-        bool overflow = false;
+        int clear_n = 1;
         if (lane == 0) {
-            top.set(0, curdist, cur);
-            cand.set(0, -curdist, cur);
             atomicOr(&vis[cur >> 5], 1u << (cur & 31));
             if (a.clear_cap > 0)
                 clr[0] = (int32_t)cur;
         }
-        __syncthreads();
-        FLAT_STAMP(0); // query setup + upper levels
-        // row of the predicted next candidate, loaded while lane 0 works the heaps (maxM0 <= 128)
+        // row of the predicted next candidate, loaded during the bookkeeping of this hop (maxM0 <= 128)
         uint32_t pf_c = ~0u, pf_w0 = 0u, pf_w1 = 0u;
         int pf_cnt = 0;
         const bool narrow = a.maxM0 <= 128;
-        const bool top_par = a.ef + 1 <= a.top_lds; // top_candidates entirely in LDS
-        while (cand_len > 0) {
-            const float cdist = -cand.key(0);
-            if (cdist > lowerBound)
-                break;
-            const uint32_t c = cand.id(0);
-            __syncthreads();
-            if (cand_len > 1) {
-                if (cand_len <= a.cand_lds) {
-                    par_pop_any(cdk, cdi, cand_len);
-                } else {
-                    if (lane == 0)
-                        stl_pop(cand, cand_len);
-                    __syncthreads();
-                }
-            }
-            cand_len--;
-            nhops++;
-            FLAT_STAMP(1); // candidate_set pop
-            // the row of c: maxM0 links, lane j holds links j, j + 64, ...
-            const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
-            int cnt;
-            uint32_t r0, r1;
-            if (c == pf_c) {
-                cnt = pf_cnt;
-                r0 = pf_w0;
-                r1 = pf_w1;
-            } else {
-                cnt = (int)(a.l0cnt[c] & 0xFFFFu);
-                r0 = row[min(lane, a.maxM0 - 1)];
-                r1 = row[min(64 + lane, a.maxM0 - 1)];
-            }
-            const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-            int nf = 0;
-            for (int base = 0; base < cnt; base += 128) { // one pass when maxM0 <= 128
-                const int j0 = base + lane, j1 = base + 64 + lane;
-                const bool act0 = j0 < cnt, act1 = j1 < cnt;
-                const uint32_t v0 = base == 0 ? r0 : row[min(j0, a.maxM0 - 1)];
-                const uint32_t v1 = base == 0 ? r1 : row[min(j1, a.maxM0 - 1)];
-                const uint32_t b0 = 1u << (v0 & 31), b1 = 1u << (v1 & 31);
-                uint32_t o0 = ~0u, o1 = ~0u;
-                if (act0)
-                    o0 = atomicOr(&vis[v0 >> 5], b0);
-                if (act1)
-                    o1 = atomicOr(&vis[v1 >> 5], b1);
-                bool fresh0 = (o0 & b0) == 0u, fresh1 = (o1 & b1) == 0u;
-                if (a.check_dups) { // a repeated link in one row: only its first occurrence is fresh
-                    for (int jj = 0; jj < cnt; ++jj) {
-                        const uint32_t vj = row[jj];
-                        fresh0 = fresh0 && !(jj < j0 && vj == v0);
-                        fresh1 = fresh1 && !(jj < j1 && vj == v1);
-                    }
-                }
-                const uint64_t fm0 = __ballot(fresh0), fm1 = __ballot(fresh1);
-                const int n0 = __popcll(fm0);
-                if (fresh0) {
-                    const int p = nf + __popcll(fm0 & below);
-                    fid[p] = v0;
-                    if (clear_n + p < a.clear_cap)
-                        clr[clear_n + p] = (int32_t)v0;
-                }
-                if (fresh1) {
-                    const int p = nf + n0 + __popcll(fm1 & below);
-                    fid[p] = v1;
-                    if (clear_n + p < a.clear_cap)
-                        clr[clear_n + p] = (int32_t)v1;
-                }
-                nf += n0 + __popcll(fm1);
-            }
-            clear_n += nf;
-            __syncthreads();
-            FLAT_STAMP(2); // row + visited
-            l2_dispatch<NV>(a, q, qr, fid, nf, fd);
-            ndis += nf;
-            FLAT_STAMP(3); // distances
-            if (narrow) {
-                // next pop = the nearer of the candidate_set root and the nearest fresh item that
-                // passes the current bound; issue its row loads now, consume them next hop
-                float bd = INFINITY;
-                int bf = 0x7FFFFFFF;
-                for (int f = lane; f < nf; f += 64) {
-                    const float d = fd[f];
-                    if (d < bd) {
-                        bd = d;
-                        bf = f;
-                    }
-                }
+        bool keep = true; // false: handed to the exact pass (NR > 0)
+        int nres = 0;
+        if constexpr (NR > 0) {
+            // Tie-free fast path. While no two entries of top_candidates share a distance:
+            //  * top_candidates is a sorted array (entry e in register e >> 6 of lane e & 63), and
+            //    pop() drops its last entry -- there is one maximum, so the heap layout is moot;
+            //  * candidate_set holds exactly the entries of top not yet expanded, plus entries
+            //    evicted from top, whose distance then exceeds lowerBound for good (strictly, as the
+            //    evicted maximum was unique): they can only trigger `cdist > lowerBound`, which is
+            //    reached exactly when no unexpanded entry is left. So candidate_set.top() is the
+            //    first unexpanded entry (unique minimum), marked by bit 31 of its id once expanded.
+            // The first equal distance among top's entries hands the query to the exact pass.
+            float tk[NR];
+            uint32_t ti[NR];
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    const float od = __shfl_xor(bd, off);
-                    const int of = __shfl_xor(bf, off);
-                    if (od < bd || (od == bd && of < bf)) {
-                        bd = od;
-                        bf = of;
-                    }
-                }
-                const float croot = cand_len > 0 ? -cand.key(0) : INFINITY;
-                uint32_t pred = ~0u;
-                if (bf < nf && (top_len < a.ef || bd < lowerBound) && bd < croot)
-                    pred = fid[bf];
-                else if (cand_len > 0)
-                    pred = cand.id(0);
-                pred = __builtin_amdgcn_readfirstlane(pred);
-                if (pred != ~0u && pred != pf_c) {
-                    const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
-                    pf_c = pred;
-                    pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
-                    pf_w0 = prow[min(lane, a.maxM0 - 1)];
-                    pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
-                }
+            for (int r = 0; r < NR; ++r) {
+                tk[r] = INFINITY;
+                ti[r] = 0u;
             }
-            // consideration in link order: `if (top.size() < ef || lowerBound > dist)` push both heaps,
-            // trim top to ef. lowerBound only falls once top is full, so one ballot per 64 links
-            // picks a superset of the accepted ones and only those are visited (exact test rechecked).
-            for (int base = 0; base < nf; base += 64) {
-                const int f = base + lane;
-                const float dl = f < nf ? fd[f] : INFINITY;
-                const uint32_t il = f < nf ? fid[f] : 0u;
-                uint64_t mask = __ballot(f < nf && (top_len < a.ef || lowerBound > dl));
-                while (mask) {
-                    const int b = __builtin_ctzll(mask);
-                    mask &= mask - 1;
-                    const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
-                    if (!(top_len < a.ef || lowerBound > dist))
-                        continue;
-                    if (cand_len >= cand_cap) {
-                        overflow = true;
-                        break;
+            if (lane == 0) {
+                tk[0] = curdist;
+                ti[0] = cur;
+            }
+            int tsz = 1;
+            float lb = curdist;
+            FLAT_STAMP(0); // query setup + upper levels
+            for (;;) {
+                int e = -1;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint64_t m = __ballot(64 * r + lane < tsz && !(ti[r] >> 31));
+                    if (e < 0 && m)
+                        e = 64 * r + __builtin_ctzll(m);
+                }
+                if (e < 0)
+                    break;
+                uint32_t c = 0;
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    if ((e >> 6) == r) {
+                        c = __builtin_amdgcn_readlane(ti[r], e & 63);
+                        if (lane == (e & 63))
+                            ti[r] |= 0x80000000u;
                     }
-                    const uint32_t id = __builtin_amdgcn_readlane(il, b);
-                    if (++cand_len <= a.cand_lds) {
-                        par_push(cdk, cdi, cand_len, -dist, id);
-                    } else {
-                        if (lane == 0) {
-                            cand.set(cand_len - 1, -dist, id);
-                            stl_push(cand, cand_len, -dist, id);
-                        }
-                        __syncthreads();
+                nhops++;
+                FLAT_STAMP(1); // next candidate
+                const int nf = expand_row(a, c, vis, clr, clear_n, fid, c == pf_c, pf_cnt, pf_w0, pf_w1);
+                clear_n += nf;
+                FLAT_STAMP(2); // row + visited
+                l2_dispatch<NV>(a, q, qr, fid, nf, fd);
+                ndis += nf;
+                FLAT_STAMP(3); // distances
+                if (narrow) { // next expansion: the first unexpanded entry, or a nearer accepted link
+                    int bf;
+                    const float bd = nearest_fresh(fd, nf, bf);
+                    int e2 = -1;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        const uint64_t m = __ballot(64 * r + lane < tsz && !(ti[r] >> 31));
+                        if (e2 < 0 && m)
+                            e2 = 64 * r + __builtin_ctzll(m);
                     }
-                    ++top_len;
-                    if (top_par) {
-                        if (par_push(topk, topi, top_len, dist, id))
-                            lowerBound = dist;
-                        while (top_len > a.ef)
-                            lowerBound = par_pop_any(topk, topi, top_len--);
-                    } else {
-                        if (lane == 0) {
-                            top.set(top_len - 1, dist, id);
-                            stl_push(top, top_len, dist, id);
-                            int tl = top_len;
-                            while (tl > a.ef)
-                                stl_pop(top, tl--);
-                            sh[2] = __float_as_int(top.key(0));
+                    float ek = INFINITY;
+                    uint32_t eid = ~0u;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r)
+                        if (e2 >= 0 && (e2 >> 6) == r) {
+                            ek = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(tk[r]), e2 & 63));
+                            eid = __builtin_amdgcn_readlane(ti[r], e2 & 63);
                         }
-                        __syncthreads();
-                        top_len = min(top_len, a.ef);
-                        lowerBound = __int_as_float(sh[2]);
+                    uint32_t pred = eid;
+                    if (bf < nf && (tsz < a.ef || bd < lb) && bd < ek)
+                        pred = fid[bf];
+                    pred = __builtin_amdgcn_readfirstlane(pred);
+                    if (pred != ~0u && pred != pf_c) {
+                        const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
+                        pf_c = pred;
+                        pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
+                        pf_w0 = prow[min(lane, a.maxM0 - 1)];
+                        pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
                     }
                 }
+                // consideration in link order: insert each accepted link by rank
+                for (int base = 0; base < nf && keep; base += 64) {
+                    const int f = base + lane;
+                    const float dl = f < nf ? fd[f] : INFINITY;
+                    const uint32_t il = f < nf ? fid[f] : 0u;
+                    uint64_t mask = __ballot(f < nf && (tsz < a.ef || lb > dl));
+                    while (mask) {
+                        const int b = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
+                        if (!(tsz < a.ef || lb > dist))
+                            continue;
+                        const uint32_t id = __builtin_amdgcn_readlane(il, b);
+                        int rank = 0;
+                        uint64_t eq = 0;
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            const bool valid = 64 * r + lane < tsz;
+                            rank += __popcll(__ballot(valid && tk[r] < dist));
+                            eq |= __ballot(valid && tk[r] == dist);
+                        }
+                        if (eq) {
+                            keep = false;
+                            break;
+                        }
+                        float nk[NR];
+                        uint32_t ni[NR];
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            uint32_t sk = dpp_wave_shr1(__float_as_uint(tk[r]));
+                            uint32_t si = dpp_wave_shr1(ti[r]);
+                            if (r > 0 && lane == 0) {
+                                sk = __builtin_amdgcn_readlane(__float_as_uint(tk[r - 1]), 63);
+                                si = __builtin_amdgcn_readlane(ti[r - 1], 63);
+                            }
+                            const int ee = 64 * r + lane;
+                            nk[r] = ee < rank ? tk[r] : (ee == rank ? dist : __uint_as_float(sk));
+                            ni[r] = ee < rank ? ti[r] : (ee == rank ? id : si);
+                        }
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            tk[r] = nk[r];
+                            ti[r] = ni[r];
+                        }
+                        if (tsz < a.ef)
+                            tsz++;
+#pragma unroll
+                        for (int r = 0; r < NR; ++r)
+                            if (((tsz - 1) >> 6) == r)
+                                lb = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(tk[r]), (tsz - 1) & 63));
+                    }
+                }
+                __syncthreads();
+                FLAT_STAMP(4); // consideration
+                if (!keep)
+                    break;
+            }
+            if (keep) {
+                // no ties: the k smallest in ascending order are also the (dist, label) order
+                nres = min(tsz, a.k);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const int ee = 64 * r + lane;
+                    if (ee < nres) {
+                        Dq[ee] = tk[r];
+                        Lq[ee] = a.labels[ti[r] & 0x7FFFFFFFu];
+                    }
+                }
+            } else if (lane == 0) {
+                a.fb_list[atomicAdd(a.fb_count, 1u)] = qi;
+            }
+        } else {
+            int top_len = 1, cand_len = 1;
+            float lowerBound = curdist;
+            bool overflow = false;
+            if (lane == 0) {
+                top.set(0, curdist, cur);
+                cand.set(0, -curdist, cur);
+            }
+            __syncthreads();
+            FLAT_STAMP(0); // query setup + upper levels
+            const bool top_par = a.ef + 1 <= min(a.top_lds, 513); // top_candidates in LDS, parallel ops
+            while (cand_len > 0) {
+                const float cdist = -cand.key(0);
+                if (cdist > lowerBound)
+                    break;
+                const uint32_t c = cand.id(0);
+                __syncthreads();
+                if (cand_len > 1) {
+                    if (cand_len <= a.cand_lds) {
+                        par_pop_any(cdk, cdi, cand_len);
+                    } else {
+                        if (lane == 0)
+                            stl_pop(cand, cand_len);
+                        __syncthreads();
+                    }
+                }
+                cand_len--;
+                nhops++;
+                FLAT_STAMP(1); // candidate_set pop
+                const int nf = expand_row(a, c, vis, clr, clear_n, fid, c == pf_c, pf_cnt, pf_w0, pf_w1);
+                clear_n += nf;
+                FLAT_STAMP(2); // row + visited
+                l2_dispatch<NV>(a, q, qr, fid, nf, fd);
+                ndis += nf;
+                FLAT_STAMP(3); // distances
+                if (narrow) { // next pop: the candidate_set root, or a nearer link passing the bound
+                    int bf;
+                    const float bd = nearest_fresh(fd, nf, bf);
+                    const float croot = cand_len > 0 ? -cand.key(0) : INFINITY;
+                    uint32_t pred = ~0u;
+                    if (bf < nf && (top_len < a.ef || bd < lowerBound) && bd < croot)
+                        pred = fid[bf];
+                    else if (cand_len > 0)
+                        pred = cand.id(0);
+                    pred = __builtin_amdgcn_readfirstlane(pred);
+                    if (pred != ~0u && pred != pf_c) {
+                        const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
+                        pf_c = pred;
+                        pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
+                        pf_w0 = prow[min(lane, a.maxM0 - 1)];
+                        pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
+                    }
+                }
+                // consideration in link order: `if (top.size() < ef || lowerBound > dist)` push both
+                // heaps, trim top to ef. lowerBound only falls once top is full, so one ballot per 64
+                // links picks a superset of the accepted ones (the exact test is rechecked).
+                for (int base = 0; base < nf; base += 64) {
+                    const int f = base + lane;
+                    const float dl = f < nf ? fd[f] : INFINITY;
+                    const uint32_t il = f < nf ? fid[f] : 0u;
+                    uint64_t mask = __ballot(f < nf && (top_len < a.ef || lowerBound > dl));
+                    while (mask) {
+                        const int b = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
+                        if (!(top_len < a.ef || lowerBound > dist))
+                            continue;
+                        if (cand_len >= cand_cap) {
+                            overflow = true;
+                            break;
+                        }
+                        const uint32_t id = __builtin_amdgcn_readlane(il, b);
+                        if (++cand_len <= a.cand_lds) {
+                            par_push(cdk, cdi, cand_len, -dist, id);
+                        } else {
+                            if (lane == 0) {
+                                cand.set(cand_len - 1, -dist, id);
+                                stl_push(cand, cand_len, -dist, id);
+                            }
+                            __syncthreads();
+                        }
+                        ++top_len;
+                        if (top_par) {
+                            if (par_push(topk, topi, top_len, dist, id))
+                                lowerBound = dist;
+                            while (top_len > a.ef)
+                                lowerBound = par_pop_any(topk, topi, top_len--);
+                        } else {
+                            if (lane == 0) {
+                                top.set(top_len - 1, dist, id);
+                                stl_push(top, top_len, dist, id);
+                                int tl = top_len;
+                                while (tl > a.ef)
+                                    stl_pop(top, tl--);
+                                sh[2] = __float_as_int(top.key(0));
+                            }
+                            __syncthreads();
+                            top_len = min(top_len, a.ef);
+                            lowerBound = __int_as_float(sh[2]);
+                        }
+                    }
+                    if (overflow)
+                        break;
+                }
+                __syncthreads();
+                FLAT_STAMP(4); // consideration: heap pushes / pops
                 if (overflow)
                     break;
             }
+            if (lane == 0 && overflow)
+                atomicAdd(a.counter + 1, 1u); // candidate_set overflow: reported by the host entry points
+            // --- while (top.size() > k) top.pop(); then order survivors by (dist, label)
+            if (top_par) {
+                while (top_len > a.k)
+                    par_pop_any(topk, topi, top_len--);
+            } else {
+                if (lane == 0) {
+                    int tl = top_len;
+                    while (tl > a.k)
+                        stl_pop(top, tl--);
+                }
+                top_len = min(top_len, a.k);
+            }
             __syncthreads();
-            FLAT_STAMP(4); // consideration: heap pushes / pops
-            if (overflow)
-                break;
+            nres = top_len;
+            // searchKnnCloserFirst order: ascending (dist, label) -- rank by counting, labels staged
+            // in the (now idle) candidate-heap LDS when they fit
+            uint64_t *lab = reinterpret_cast<uint64_t *>(cdk);
+            const bool staged = nres <= a.cand_lds;
+            if (staged)
+                for (int e = lane; e < nres; e += 64)
+                    lab[e] = a.labels[top.id(e)];
+            __syncthreads();
+            for (int e = lane; e < nres; e += 64) {
+                const float de = top.key(e);
+                const uint64_t le = staged ? lab[e] : a.labels[top.id(e)];
+                int rank = 0;
+                for (int o = 0; o < nres; ++o) {
+                    const float dq = top.key(o);
+                    const uint64_t lo = staged ? lab[o] : a.labels[top.id(o)];
+                    rank += (dq < de) || (dq == de && lo < le);
+                }
+                Dq[rank] = de;
+                Lq[rank] = le;
+            }
         }
-        if (lane == 0 && overflow)
-            atomicAdd(a.counter + 1, 1u); // candidate_set overflow: reported by the host entry points
-        // --- while (top.size() > k) top.pop(); then order survivors by (dist, label)
-        if (top_par) {
-            while (top_len > a.k)
-                par_pop_any(topk, topi, top_len--);
-        } else {
+        if (keep) {
+            for (int j = nres + lane; j < a.k; j += 64) {
+                Dq[j] = INFINITY;
+                Lq[j] = ~0ull;
+            }
             if (lane == 0) {
-                int tl = top_len;
-                while (tl > a.k)
-                    stl_pop(top, tl--);
+                a.ndis[qi] = ndis;
+                a.nhops[qi] = nhops;
+                if (a.nhops_upper)
+                    a.nhops_upper[qi] = nhops_up;
             }
-            top_len = min(top_len, a.k);
-        }
-        __syncthreads();
-        const int nres = top_len;
-        // searchKnnCloserFirst order: ascending (dist, label) -- rank by counting, labels staged in
-        // the (now idle) candidate-heap LDS when they fit
-        uint64_t *lab = reinterpret_cast<uint64_t *>(cdk);
-        const bool staged = nres <= a.cand_lds;
-        if (staged)
-            for (int e = lane; e < nres; e += 64)
-                lab[e] = a.labels[top.id(e)];
-        __syncthreads();
-        for (int e = lane; e < nres; e += 64) {
-            const float de = top.key(e);
-            const uint64_t le = staged ? lab[e] : a.labels[top.id(e)];
-            int rank = 0;
-            for (int o = 0; o < nres; ++o) {
-                const float dq = top.key(o);
-                const uint64_t lo = staged ? lab[o] : a.labels[top.id(o)];
-                rank += (dq < de) || (dq == de && lo < le);
-            }
-            Dq[rank] = de;
-            Lq[rank] = le;
-        }
-        for (int j = nres + lane; j < a.k; j += 64) {
-            Dq[j] = INFINITY;
-            Lq[j] = ~0ull;
-        }
-        if (lane == 0) {
-            a.ndis[qi] = ndis;
-            a.nhops[qi] = nhops;
-            if (a.nhops_upper)
-                a.nhops_upper[qi] = nhops_up;
         }
         // VisitedTable reset: clear exactly the bits this query set
         if (clear_n <= a.clear_cap) {
@@ -738,18 +924,55 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.top_ovf_k = ix.top_ovf_k;
     a.top_ovf_i = ix.top_ovf_i;
     a.top_ovf_cap = ix.top_ovf_cap;
-    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 2 * sizeof(uint32_t), stream));
+    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 4 * sizeof(uint32_t), stream));
     a.stamps = ix.stamps;
+    a.qlist = nullptr;
+    a.qcount = nullptr;
+    // pass 1 (opt-in, DRM_SEARCH_SORTED=1): the tie-free sorted-array kernel (ef <= 256, d = 128,
+    // ids < 2^31); the queries that meet a distance tie go to fb_list and pass 2 (the exact heap
+    // replay) redoes them. Off by default: the 3-mer stand-in embedding maps shifted windows onto
+    // identical vectors so often that ~89 % of C3 queries meet a tie (oracle count).
+    const int nr = efc <= 64 ? 1 : efc <= 128 ? 2 : efc <= 256 ? 4 : 0;
+    const bool sorted_pass = ix.try_sorted && ix.d == 128 && nr > 0 && ix.ntotal < 0x7FFFFFFFll;
+    if (sorted_pass) {
+        if (n > ix.fb_cap) {
+            if (ix.fb_list)
+                DRM_HIP_CHECK(hipFree(ix.fb_list));
+            ix.fb_list = nullptr;
+            DRM_HIP_CHECK(hipMalloc(&ix.fb_list, sizeof(int32_t) * (size_t)n));
+            ix.fb_cap = n;
+        }
+        a.fb_list = ix.fb_list;
+        a.fb_count = ix.counter + 2;
+#define DRM_FLAT_SORTED(NR_)                                                                                   \
+    if (ix.stamps)                                                                                              \
+        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, NR_, true>), dim3(slots), dim3(64), lds, stream, a);    \
+    else                                                                                                        \
+        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, NR_, false>), dim3(slots), dim3(64), lds, stream, a);
+        if (nr == 1) {
+            DRM_FLAT_SORTED(1)
+        } else if (nr == 2) {
+            DRM_FLAT_SORTED(2)
+        } else {
+            DRM_FLAT_SORTED(4)
+        }
+#undef DRM_FLAT_SORTED
+        DRM_HIP_CHECK(hipGetLastError());
+        a.qlist = ix.fb_list;
+        a.qcount = ix.counter + 2;
+        a.counter = ix.counter + 3;
+        a.stamps = nullptr;
+    }
     if (ix.d == 128) {
-        if (ix.stamps)
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, true>), dim3(slots), dim3(64), lds, stream, a);
+        if (a.stamps)
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, true>), dim3(slots), dim3(64), lds, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, false>), dim3(slots), dim3(64), lds, stream, a);
     } else {
-        if (ix.stamps)
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, true>), dim3(slots), dim3(64), lds, stream, a);
+        if (a.stamps)
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, true>), dim3(slots), dim3(64), lds, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, false>), dim3(slots), dim3(64), lds, stream, a);
     }
     DRM_HIP_CHECK(hipGetLastError());
 }

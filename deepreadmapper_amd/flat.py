@@ -56,6 +56,12 @@ class HnswFlatIndex:
         check(lib().drm_flat_search_overflows(self.handle, C.byref(c)))
         return int(c.value)
 
+    def fallbacks(self):
+        """Queries of the last search redone by the exact heap-replay pass (distance ties)."""
+        c = C.c_int64(0)
+        check(lib().drm_flat_search_fallbacks(self.handle, C.byref(c)))
+        return int(c.value)
+
     def free(self):
         if self._h:
             check(lib().drm_flat_index_free(self._h))

@@ -135,6 +135,9 @@ int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, i
 /* Diagnostic: queries of the last search whose candidate_set outgrew the GPU heap (their outputs
  * are invalid; drm_flat_search reports it as an error). Synchronizes the device. */
 int drm_flat_search_overflows(drm_flat_index *index, int64_t *count);
+/* Diagnostic: queries of the last search that the tie-free sorted-array pass handed to the exact
+ * heap-replay pass (a distance tie among top_candidates). Synchronizes the device. */
+int drm_flat_search_fallbacks(drm_flat_index *index, int64_t *count);
 
 /* ---------------------------------------------------------------- Smith-Waterman rerank */
 /* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):

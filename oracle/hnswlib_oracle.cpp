@@ -34,6 +34,7 @@
 
 namespace {
 thread_local size_t t_maxcand = 0; // diagnostic: largest candidate_set of the thread's queries
+thread_local int64_t t_tieq[3] = {0, 0, 0}; // diagnostic: queries with a tied eviction / tied pop / any
 
 struct Flat {
     int d;
@@ -116,6 +117,7 @@ void search_one(const Flat &ix, const float *q, int k, int ef_, float *D, int64_
         tag = 1;
     }
     PQ top, cand;
+    bool tie_evict = false, tie_pop = false;
     float lowerBound = curdist;
     top.emplace(curdist, cur);
     cand.emplace(-curdist, cur);
@@ -128,6 +130,8 @@ void search_one(const Flat &ix, const float *q, int k, int ef_, float *D, int64_
         if (cand.size() > t_maxcand)
             t_maxcand = cand.size();
         cand.pop();
+        if (!cand.empty() && cand.top().first == cp.first)
+            tie_pop = true;
         nhops++;
         const uint32_t *row = ix.l0 + (size_t)cp.second * (1 + ix.maxM0);
         const int size = (int)(row[0] & 0xFFFFu);
@@ -141,13 +145,20 @@ void search_one(const Flat &ix, const float *q, int k, int ef_, float *D, int64_
             if (top.size() < ef || lowerBound > dist) {
                 cand.emplace(-dist, c);
                 top.emplace(dist, c);
-                while (top.size() > ef)
+                while (top.size() > ef) {
+                    const float ev = top.top().first;
                     top.pop();
+                    if (top.top().first == ev)
+                        tie_evict = true;
+                }
                 if (!top.empty())
                     lowerBound = top.top().first;
             }
         }
     }
+    t_tieq[0] += tie_evict;
+    t_tieq[1] += tie_pop;
+    t_tieq[2] += tie_evict || tie_pop;
     while (top.size() > (size_t)k)
         top.pop();
     std::priority_queue<std::pair<float, uint64_t>> result;
@@ -174,6 +185,14 @@ void search_one(const Flat &ix, const float *q, int k, int ef_, float *D, int64_
 extern "C" {
 
 static size_t g_maxcand = 0;
+static int64_t g_tieq[3] = {0, 0, 0};
+// diagnostic: queries of the last oracle_hnswlib_search call with a tie at an eviction of
+// top_candidates / at a candidate_set pop / either (where heap layouts decide the traversal)
+void oracle_hnswlib_tie_queries(int64_t *out3)
+{
+    for (int i = 0; i < 3; ++i)
+        out3[i] = g_tieq[i];
+}
 // diagnostic: the largest candidate_set size seen by the last oracle_hnswlib_search call
 size_t oracle_hnswlib_maxcand() { return g_maxcand; }
 
@@ -189,6 +208,7 @@ int oracle_hnswlib_search(int d, int64_t ntotal, int maxM0, int maxM, int maxlev
         return -1;
     Flat ix{d, ntotal, maxM0, maxM, maxlevel, ep, vec, l0, up_off, up, labels};
     g_maxcand = 0;
+    g_tieq[0] = g_tieq[1] = g_tieq[2] = 0;
 #ifdef _OPENMP
     if (nthreads <= 0)
         nthreads = omp_get_max_threads();
@@ -198,6 +218,7 @@ int oracle_hnswlib_search(int d, int64_t ntotal, int maxM0, int maxM, int maxlev
         std::vector<uint32_t> vis((size_t)(ntotal > 0 ? ntotal : 1), 0u);
         uint32_t tag = 0;
         t_maxcand = 0;
+        t_tieq[0] = t_tieq[1] = t_tieq[2] = 0;
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif
@@ -206,7 +227,11 @@ int oracle_hnswlib_search(int d, int64_t ntotal, int maxM0, int maxM, int maxlev
 #ifdef _OPENMP
 #pragma omp critical
 #endif
-        g_maxcand = std::max(g_maxcand, t_maxcand);
+        {
+            g_maxcand = std::max(g_maxcand, t_maxcand);
+            for (int i = 0; i < 3; ++i)
+                g_tieq[i] += t_tieq[i];
+        }
     }
     return 0;
 }
