@@ -29,6 +29,15 @@ namespace {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+// The lane id as an opaque value: per-lane index arithmetic derived from it is recomputed where it
+// is used instead of being hoisted out of the hop loop, where it would pin VGPRs (occupancy).
+__device__ __forceinline__ int lane_id_local()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // Heap array accessor: LDS part, plus (OVF) a per-slot global continuation past lds_cap entries.
 template <bool OVF> struct HeapRef {
     float *k;         // LDS keys [lds_cap]
@@ -107,7 +116,7 @@ __device__ __forceinline__ int heap_depth(int slot) { return 31 - __builtin_clz(
 // Returns true when vk became the root.
 __device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float vk, uint32_t vi)
 {
-    const int lane = lane_id();
+    const int lane = lane_id_local();
     const int hole = len - 1;
     const int m = heap_depth(hole);
     const int j = lane + 1;
@@ -139,7 +148,7 @@ __device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float v
 // walk over those bits. NN = node groups (L <= 128 NN + 1). Returns the new root key.
 template <int NN> __device__ __forceinline__ float par_pop(float *K, uint32_t *I, int len)
 {
-    const int lane = lane_id();
+    const int lane = lane_id_local();
     const int L = len - 1;
     const float vk = K[L];
     const uint32_t vi = I[L];
@@ -241,12 +250,19 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 // Same distances with the query slice in registers (qr[r] = q[sub + 8r], NV = d / 8 per lane) and
 // every load of a pass issued before the first use: 16 items per pass, two per lane group, so a
 // hop's distances cost one memory round trip instead of one per dimension step.
+#ifndef DRM_FLAT_Q_REGS
+#define DRM_FLAT_Q_REGS 1 // 1: the query slice stays in 16 VGPRs; 0: re-read from LDS per pass (occupancy)
+#endif
 template <int NV>
-__device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float (&qr)[NV], const uint32_t *ids,
-                                             int nitem, float *out)
+__device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float *q, const float (&qreg)[NV],
+                                             const uint32_t *ids, int nitem, float *out)
 {
-    const int lane = lane_id(), grp = lane >> 3, sub = lane & 7;
+    const int lane = lane_id_local(), grp = lane >> 3, sub = lane & 7;
     for (int base = 0; base < nitem; base += 16) {
+        float qr[NV];
+#pragma unroll
+        for (int r = 0; r < NV; ++r)
+            qr[r] = DRM_FLAT_Q_REGS ? qreg[r] : q[sub + 8 * r];
         const int f0 = base + grp, f1 = base + 8 + grp;
         const bool two = base + 8 < nitem; // wave-uniform
         const float *v0 = a.vec + (size_t)ids[min(f0, nitem - 1)] * (size_t)(8 * NV) + sub;
@@ -300,7 +316,7 @@ __device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, c
                                             const uint32_t *ids, int nitem, float *out)
 {
     if constexpr (NV > 0)
-        l2_items_reg<NV>(a, qr, ids, nitem, out);
+        l2_items_reg<NV>(a, q, qr, ids, nitem, out);
     else
         l2_items(a, q, ids, nitem, out);
 }
@@ -310,7 +326,7 @@ __device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, c
 __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_t *vis, int32_t *clr, int clear_n,
                                           uint32_t *fid, bool have_pf, int pf_cnt, uint32_t pf_w0, uint32_t pf_w1)
 {
-    const int lane = lane_id();
+    const int lane = lane_id_local();
     const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
     int cnt;
     uint32_t r0, r1;
@@ -367,7 +383,7 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
 // Nearest fresh item that passes the current bound (wave argmin over fd[0 .. nf)); +inf if none.
 __device__ __forceinline__ float nearest_fresh(const float *fd, int nf, int &bf)
 {
-    const int lane = lane_id();
+    const int lane = lane_id_local();
     float bd = INFINITY;
     bf = 0x7FFFFFFF;
     for (int f = lane; f < nf; f += 64) {
@@ -409,7 +425,7 @@ __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
 // NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
 // NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
 template <int NV, int NR, bool STAMPS>
-__global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
@@ -458,7 +474,7 @@ __global__ __launch_bounds__(64) void hnsw_flat_search_kernel(FlatArgs a)
             continue;
         }
         float qr[NV > 0 ? NV : 1];
-        if constexpr (NV > 0) {
+        if constexpr (NV > 0 && DRM_FLAT_Q_REGS) {
 #pragma unroll
             for (int r = 0; r < NV; ++r)
                 qr[r] = a.x[(int64_t)qi * a.d + (lane & 7) + 8 * r];
