@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
-"""bench.py -- mapped reads/s of the MI355X hot path (HNSW-PQ search + SW rerank, EF=128, K=128).
+"""bench.py -- mapped reads/s of the MI355X hot path (HNSW search + SW rerank, EF=128, K=128).
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`; N>1 is launched by
 torch.distributed.run, one rank per GPU. One step = one pass of the hot path over this rank's batch
-of synthetic 150 bp reads, inputs already resident in HBM: the HNSW-PQ search kernel
-(faiss_search(index, emb, k_clusters=K, ef=EF), src/main.cpp:278) followed by the SW rerank kernel
-(post_process_sw_static(..., k=K, k_clusters=K), src/main.cpp:340). Rank 0 prints ONE JSON line.
+of synthetic 150 bp reads, inputs already resident in HBM: the HNSW search kernel followed by the SW
+rerank kernel (post_process_sw_static(..., k=K, k_clusters=K), src/main.cpp:340). Rank 0 prints ONE
+JSON line.
 
-Workload (BASELINE.json configs[2] "C3"): a seeded 500,149 bp genome, stride-1
-dense index of 1,000,000 fwd/RC 150 bp windows (IndexHNSWPQ M_pq=8 nbits=8 M_hnsw=16 EFC=200, built
-here since faiss is absent), 100,000 reads per GPU (1 % substitutions; weak scaling: the per-GPU batch
-is fixed). Queries are embedded with the 3-mer stand-in (the OpenVINO encoder is out of scope); the
-reference's timed "Search time" window likewise excludes inference (src/main.cpp:272-285).
+Search (`--index`):
+  flat (default): BASELINE.json configs[1]'s "HIP L2 HNSW search" -- hnswlib fp32-L2 searchKnn
+      (search(index, queries, k, ef), src/hnswlib_dir/search.cpp:7-52) on an hnswlib index with the
+      reference's defaults M=64, EFC=128 (src/hnswlib_dir/index.cpp); the distance kernel whose HBM
+      roofline the north star quotes (512 B per distance).
+  pq: faiss IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200, built here since faiss is absent) through
+      faiss_search(index, emb, k_clusters=K, ef=EF) (src/main.cpp:278), the live pipeline's index.
+
+Workload (BASELINE.json configs[2] "C3", the HBM-roofline run): a seeded 500,149
+bp genome, stride-1 dense window table of 1,000,000 fwd/RC 150 bp windows, 100,000 reads per GPU (1 %
+substitutions; weak scaling: the per-GPU batch is fixed). Queries are embedded with the 3-mer
+stand-in (the OpenVINO encoder is out of scope); the reference's timed "Search time" window likewise
+excludes inference (src/main.cpp:272-285).
 """
 import argparse
 import json
@@ -27,7 +35,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
 SEARCH_KERNEL = "hnsw_pq_search_kernel<2, true, 0, true, false>"  # what C3 (ef = k = 128, PQ8x8) launches
-FLAT_KERNEL = "hnsw_flat_search_kernel"  # --index flat
+FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<152>"
 SW_VALU_PER_CELL = 556 / 152 / 2  # static ISA count of the sw_score_f16_kernel<152> row loop: 556 VALU per 152 cell pairs
 
@@ -278,9 +286,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--build-threads", type=int, default=0)
-    ap.add_argument("--index", choices=["pq", "flat"], default="pq",
-                    help="pq (default): faiss IndexHNSWPQ, the live pipeline's index; flat: hnswlib fp32-L2 "
-                         "index (M=64, EFC=128, the reference's hnswlib defaults) over the same windows")
+    ap.add_argument("--index", choices=["pq", "flat"], default="flat",
+                    help="flat (default): hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib "
+                         "defaults), configs[1]'s L2 HNSW search; pq: faiss IndexHNSWPQ, the live pipeline's index")
     ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
                     help="c3 (default, the headline): search + SW rerank; c4: search only on a 10M-vector "
                          "sparse (stride 4) index, SURVEY.md sec. 8d")

@@ -250,6 +250,9 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 // Same distances with the query slice in registers (qr[r] = q[sub + 8r], NV = d / 8 per lane) and
 // every load of a pass issued before the first use: 16 items per pass, two per lane group, so a
 // hop's distances cost one memory round trip instead of one per dimension step.
+#ifndef DRM_FLAT_TWO_SETS
+#define DRM_FLAT_TWO_SETS 0 // 1: 16 items per pass (two per lane group); 0: 8 (fewer VGPRs)
+#endif
 #ifndef DRM_FLAT_Q_REGS
 #define DRM_FLAT_Q_REGS 1 // 1: the query slice stays in 16 VGPRs; 0: re-read from LDS per pass (occupancy)
 #endif
@@ -258,13 +261,13 @@ __device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float *q, 
                                              const uint32_t *ids, int nitem, float *out)
 {
     const int lane = lane_id_local(), grp = lane >> 3, sub = lane & 7;
-    for (int base = 0; base < nitem; base += 16) {
+    for (int base = 0; base < nitem; base += DRM_FLAT_TWO_SETS ? 16 : 8) {
         float qr[NV];
 #pragma unroll
         for (int r = 0; r < NV; ++r)
             qr[r] = DRM_FLAT_Q_REGS ? qreg[r] : q[sub + 8 * r];
         const int f0 = base + grp, f1 = base + 8 + grp;
-        const bool two = base + 8 < nitem; // wave-uniform
+        const bool two = DRM_FLAT_TWO_SETS && base + 8 < nitem; // wave-uniform
         const float *v0 = a.vec + (size_t)ids[min(f0, nitem - 1)] * (size_t)(8 * NV) + sub;
         const float *v1 = a.vec + (size_t)ids[min(f1, nitem - 1)] * (size_t)(8 * NV) + sub;
         float t0[NV], t1[NV];
@@ -425,7 +428,7 @@ __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
 // NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
 // NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
 template <int NV, int NR, bool STAMPS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_flat_search_kernel(FlatArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
