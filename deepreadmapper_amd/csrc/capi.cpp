@@ -440,7 +440,10 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t *row = &h.l0[(size_t)i * (1 + h.maxM0)];
             cnt[(size_t)i] = row[0] & 0xFFFFu;
-            std::memcpy(&l0[(size_t)i * d.maxM0], row + 1, sizeof(uint32_t) * d.maxM0);
+            std::memcpy(&l0[(size_t)i * d.maxM0], row + 1, sizeof(uint32_t) * cnt[(size_t)i]);
+            // slots past the count hold ~0u: the kernel's row step needs no count (ids < 2^32 - 1)
+            std::fill(l0.begin() + (int64_t)i * d.maxM0 + cnt[(size_t)i], l0.begin() + (int64_t)(i + 1) * d.maxM0,
+                      0xFFFFFFFFu);
             if (!d.has_dup_links) { // a row listing one id twice: only its first occurrence is fresh
                 std::unordered_set<uint32_t> seen;
                 for (uint32_t j = 0; j < cnt[(size_t)i]; ++j)

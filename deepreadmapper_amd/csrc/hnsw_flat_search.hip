@@ -38,20 +38,34 @@ __device__ __forceinline__ int lane_id_local()
     return l;
 }
 
+// Heap entries live in LDS as interleaved (key bits, id) pairs: one 8-byte access per entry, and a
+// node's two children (slots 2p+1, 2p+2) are one ds_read2_b64.
+typedef uint2 KV;
+__device__ __forceinline__ float kv_key(KV e) { return __uint_as_float(e.x); }
+__device__ __forceinline__ KV kv_make(float k, uint32_t i) { return make_uint2(__float_as_uint(k), i); }
+
+// Address-space-qualified pointers: an access that may go to either part stays a branch between an
+// LDS and a global instruction. Generic pointers would let the compiler fold the two into one flat_*
+// access, and flat accesses count against both vmcnt and lgkmcnt -- every LDS wait after one would
+// then also wait for the outstanding row prefetch.
+#define DRM_LDS __attribute__((address_space(3)))
+#define DRM_GLOBAL __attribute__((address_space(1)))
+
 // Heap array accessor: LDS part, plus (OVF) a per-slot global continuation past lds_cap entries.
 template <bool OVF> struct HeapRef {
-    float *k;         // LDS keys [lds_cap]
-    uint32_t *i;      // LDS ids
+    DRM_LDS uint64_t *kv;    // LDS entries [lds_cap], the KV pairs as (id << 32 | key bits)
     int lds_cap;
-    float *ok;        // overflow keys (global), OVF only
-    uint32_t *oi;     // overflow ids
-    __device__ float key(int t) const { return (!OVF || t < lds_cap) ? k[t] : ok[t - lds_cap]; }
-    __device__ uint32_t id(int t) const { return (!OVF || t < lds_cap) ? i[t] : oi[t - lds_cap]; }
+    DRM_GLOBAL float *ok;    // overflow keys (global), OVF only
+    DRM_GLOBAL uint32_t *oi; // overflow ids
+    __device__ float key(int t) const
+    {
+        return (!OVF || t < lds_cap) ? __uint_as_float((uint32_t)kv[t]) : ok[t - lds_cap];
+    }
+    __device__ uint32_t id(int t) const { return (!OVF || t < lds_cap) ? (uint32_t)(kv[t] >> 32) : oi[t - lds_cap]; }
     __device__ void set(int t, float kk, uint32_t ii) const
     {
         if (!OVF || t < lds_cap) {
-            k[t] = kk;
-            i[t] = ii;
+            kv[t] = (uint64_t)__float_as_uint(kk) | ((uint64_t)ii << 32);
         } else {
             ok[t - lds_cap] = kk;
             oi[t - lds_cap] = ii;
@@ -114,7 +128,7 @@ __device__ __forceinline__ int heap_depth(int slot) { return 31 - __builtin_clz(
 // (parent >= child), so the ancestors that move down are exactly those with key < vk: lane j reads
 // ancestor j+1, one ballot counts them (h), they shift down one level and vk lands at ancestor h.
 // Returns true when vk became the root.
-__device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float vk, uint32_t vi)
+__device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
 {
     const int lane = lane_id_local();
     const int hole = len - 1;
@@ -122,20 +136,13 @@ __device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float v
     const int j = lane + 1;
     const bool valid = j <= m;
     const int anc = valid ? ((hole + 1) >> j) - 1 : 0;
-    const float ak = K[anc];
-    const uint32_t ai = I[anc];
-    const bool lt = valid && ak < vk;
+    const KV ae = H[anc];
+    const bool lt = valid && kv_key(ae) < vk;
     const int h = __popcll(__ballot(lt));
-    if (lt) { // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
-        const int dst = ((hole + 1) >> (j - 1)) - 1;
-        K[dst] = ak;
-        I[dst] = ai;
-    }
-    if (lane == 0) {
-        const int dst = ((hole + 1) >> h) - 1;
-        K[dst] = vk;
-        I[dst] = vi;
-    }
+    if (lt) // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
+        H[((hole + 1) >> (j - 1)) - 1] = ae;
+    if (lane == 0)
+        H[((hole + 1) >> h) - 1] = kv_make(vk, vi);
     return h == m;
 }
 
@@ -145,25 +152,23 @@ __device__ __forceinline__ bool par_push(float *K, uint32_t *I, int len, float v
 // the path P_0 = root .. P_m = leaf: with h = #{i >= 1 : key(P_i) < v}, P_0 .. P_{m-h-1} each take
 // their successor's entry, P_{m-h} takes v, the rest stay. Lanes own nodes p = lane + 64 jj and hold
 // both children of p, so the child choices are one ballot per 64 nodes; the leaf is found by a scalar
-// walk over those bits. NN = node groups (L <= 128 NN + 1). Returns the new root key.
-template <int NN> __device__ __forceinline__ float par_pop(float *K, uint32_t *I, int len)
+// walk over those bits. NN = node groups (L <= 128 NN + 1). Children are read without a bounds
+// select: slots up to 128 NN stay inside the wave's LDS (the heap regions are followed by others) and
+// entries past L never take part. Returns the new root key.
+template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
 {
     const int lane = lane_id_local();
     const int L = len - 1;
-    const float vk = K[L];
-    const uint32_t vi = I[L];
-    float ck[NN];
-    uint32_t ci[NN];
+    const KV ve = H[L];
+    const float vk = kv_key(ve);
+    KV ce[NN];
     uint64_t bits[NN];
 #pragma unroll
     for (int jj = 0; jj < NN; ++jj) {
         const int p = lane + 64 * jj;
-        const bool has_l = 2 * p + 1 < L, has_r = 2 * p + 2 < L;
-        const float lk = K[has_l ? 2 * p + 1 : 0], rk = K[has_r ? 2 * p + 2 : 0];
-        const uint32_t li = I[has_l ? 2 * p + 1 : 0], ri = I[has_r ? 2 * p + 2 : 0];
-        const bool right = has_r && !(rk < lk);
-        ck[jj] = right ? rk : lk;
-        ci[jj] = right ? ri : li;
+        const KV le = H[2 * p + 1], re = H[2 * p + 2];
+        const bool right = 2 * p + 2 < L && !(kv_key(re) < kv_key(le));
+        ce[jj] = right ? re : le;
         bits[jj] = __ballot(right);
     }
     int leaf = 0;
@@ -183,32 +188,27 @@ template <int NN> __device__ __forceinline__ float par_pop(float *K, uint32_t *I
         const int p = lane + 64 * jj;
         const int dp = heap_depth(p);
         on[jj] = dp < m && (((leaf + 1) >> (m - dp)) == p + 1);
-        h += __popcll(__ballot(on[jj] && ck[jj] < vk));
+        h += __popcll(__ballot(on[jj] && kv_key(ce[jj]) < vk));
     }
     const int t = m - h; // depth where v lands
 #pragma unroll
     for (int jj = 0; jj < NN; ++jj) {
         const int p = lane + 64 * jj;
-        if (on[jj] && heap_depth(p) < t) {
-            K[p] = ck[jj];
-            I[p] = ci[jj];
-        }
+        if (on[jj] && heap_depth(p) < t)
+            H[p] = ce[jj];
     }
-    if (lane == 0) {
-        const int dst = ((leaf + 1) >> h) - 1;
-        K[dst] = vk;
-        I[dst] = vi;
-    }
-    return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ck[0]), 0)) : vk;
+    if (lane == 0)
+        H[((leaf + 1) >> h) - 1] = ve;
+    return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(ce[0].x, 0)) : vk;
 }
 
 // heaps of up to 513 entries (the callers take the serial replay beyond)
-__device__ __forceinline__ float par_pop_any(float *K, uint32_t *I, int len)
+__device__ __forceinline__ float par_pop_any(KV *H, int len)
 {
     const int L = len - 1;
     if (L <= 128)
-        return par_pop<1>(K, I, len);
-    return par_pop<4>(K, I, len);
+        return par_pop<1>(H, len);
+    return par_pop<4>(H, len);
 }
 
 __device__ __forceinline__ uint32_t dpp_row_shr1(uint32_t v)
@@ -324,31 +324,104 @@ __device__ __forceinline__ void l2_dispatch(const FlatArgs &a, const float *q, c
         l2_items(a, q, ids, nitem, out);
 }
 
-// Links of c not yet visited, in row order -> fid[0 .. nf), each marked in the visited bitmap and
-// appended to the clear list. The row's first 128 words may already be in registers (prefetch).
-__device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_t *vis, int32_t *clr, int clear_n,
-                                          uint32_t *fid, bool have_pf, int pf_cnt, uint32_t pf_w0, uint32_t pf_w1)
+// ---- Out-of-line slow paths: heaps that reach past their LDS part (candidate_set beyond cand_lds
+// entries, or top_candidates at large ef) take the serial replay on lane 0. Kept out of line so that
+// no global-memory access sits inside the common path's loops: the wait for one would also wait for
+// the outstanding row prefetch (vmcnt is in order).
+struct ConsState {
+    int top_len, cand_len;
+    float lb;
+    int overflow;
+};
+
+__device__ __forceinline__ void serial_cand_pop(HeapRef<true> cand, int len)
+{
+    if (lane_id() == 0)
+        stl_pop(cand, len);
+    __syncthreads();
+}
+
+// consideration of the fresh links from chunk `base` (remaining candidates `mask`) onward, any heap
+// sizes: the same test and heap updates as the fast loop, serial where a heap leaves LDS
+__device__ __forceinline__ ConsState slow_consider(const float *fd, const uint32_t *fid, int nf, int base0,
+                                                             uint64_t mask0, ConsState st, HeapRef<true> top,
+                                                             HeapRef<true> cand, KV *topkv, KV *cdkv, int ef,
+                                                             int cand_lds, int cand_cap, bool top_par, int *sh)
+{
+    const int lane = lane_id();
+    for (int base = base0; base < nf; base += 64) {
+        const int f = base + lane;
+        const float dl = f < nf ? fd[f] : INFINITY;
+        const uint32_t il = f < nf ? fid[f] : 0u;
+        uint64_t mask = base == base0 ? mask0 : __ballot(f < nf && (st.top_len < ef || st.lb > dl));
+        while (mask) {
+            const int b = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
+            if (!(st.top_len < ef || st.lb > dist))
+                continue;
+            if (st.cand_len >= cand_cap) {
+                st.overflow = 1;
+                return st;
+            }
+            const uint32_t id = __builtin_amdgcn_readlane(il, b);
+            if (++st.cand_len <= cand_lds) {
+                par_push(cdkv, st.cand_len, -dist, id);
+            } else {
+                if (lane == 0) {
+                    cand.set(st.cand_len - 1, -dist, id);
+                    stl_push(cand, st.cand_len, -dist, id);
+                }
+                __syncthreads();
+            }
+            ++st.top_len;
+            if (top_par) {
+                if (par_push(topkv, st.top_len, dist, id))
+                    st.lb = dist;
+                while (st.top_len > ef)
+                    st.lb = par_pop_any(topkv, st.top_len--);
+            } else {
+                if (lane == 0) {
+                    top.set(st.top_len - 1, dist, id);
+                    stl_push(top, st.top_len, dist, id);
+                    int tl = st.top_len;
+                    while (tl > ef)
+                        stl_pop(top, tl--);
+                    sh[2] = __float_as_int(top.key(0));
+                }
+                __syncthreads();
+                st.top_len = min(st.top_len, ef);
+                st.lb = __int_as_float(sh[2]);
+            }
+        }
+    }
+    return st;
+}
+
+// Links of c not yet visited, in row order -> fid[0 .. nf), each marked in the visited bitmap. Row
+// slots past the link count hold ~0u (drm_flat_index_load), so the first 128 slots need no count;
+// the caller may have issued their loads already (have_pf: pf_w0 / pf_w1 = slots lane, 64 + lane).
+__device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_t *vis, uint32_t *fid, bool have_pf,
+                                          uint32_t pf_w0, uint32_t pf_w1)
 {
     const int lane = lane_id_local();
     const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
-    int cnt;
     uint32_t r0, r1;
     if (have_pf) {
-        cnt = pf_cnt;
         r0 = pf_w0;
         r1 = pf_w1;
     } else {
-        cnt = (int)(a.l0cnt[c] & 0xFFFFu);
-        r0 = row[min(lane, a.maxM0 - 1)];
-        r1 = row[min(64 + lane, a.maxM0 - 1)];
+        r0 = lane < a.maxM0 ? row[lane] : ~0u;
+        r1 = 64 + lane < a.maxM0 ? row[64 + lane] : ~0u;
     }
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int nbase = a.maxM0 <= 128 ? 128 : (int)(a.l0cnt[c] & 0xFFFFu);
     int nf = 0;
-    for (int base = 0; base < cnt; base += 128) { // one pass when maxM0 <= 128
+    for (int base = 0; base < nbase; base += 128) { // one pass when maxM0 <= 128
         const int j0 = base + lane, j1 = base + 64 + lane;
-        const bool act0 = j0 < cnt, act1 = j1 < cnt;
-        const uint32_t v0 = base == 0 ? r0 : row[min(j0, a.maxM0 - 1)];
-        const uint32_t v1 = base == 0 ? r1 : row[min(j1, a.maxM0 - 1)];
+        const uint32_t v0 = base == 0 ? r0 : (j0 < a.maxM0 ? row[j0] : ~0u);
+        const uint32_t v1 = base == 0 ? r1 : (j1 < a.maxM0 ? row[j1] : ~0u);
+        const bool act0 = v0 != ~0u, act1 = v1 != ~0u;
         const uint32_t b0 = 1u << (v0 & 31), b1 = 1u << (v1 & 31);
         uint32_t o0 = ~0u, o1 = ~0u;
         if (act0)
@@ -357,6 +430,7 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
             o1 = atomicOr(&vis[v1 >> 5], b1);
         bool fresh0 = (o0 & b0) == 0u, fresh1 = (o1 & b1) == 0u;
         if (a.check_dups) { // a repeated link in one row: only its first occurrence is fresh
+            const int cnt = (int)(a.l0cnt[c] & 0xFFFFu);
             for (int jj = 0; jj < cnt; ++jj) {
                 const uint32_t vj = row[jj];
                 fresh0 = fresh0 && !(jj < j0 && vj == v0);
@@ -365,48 +439,25 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
         }
         const uint64_t fm0 = __ballot(fresh0), fm1 = __ballot(fresh1);
         const int n0 = __popcll(fm0);
-        if (fresh0) {
-            const int p = nf + __popcll(fm0 & below);
-            fid[p] = v0;
-            if (clear_n + p < a.clear_cap)
-                clr[clear_n + p] = (int32_t)v0;
-        }
-        if (fresh1) {
-            const int p = nf + n0 + __popcll(fm1 & below);
-            fid[p] = v1;
-            if (clear_n + p < a.clear_cap)
-                clr[clear_n + p] = (int32_t)v1;
-        }
+        if (fresh0)
+            fid[nf + __popcll(fm0 & below)] = v0;
+        if (fresh1)
+            fid[nf + n0 + __popcll(fm1 & below)] = v1;
         nf += n0 + __popcll(fm1);
     }
     __syncthreads();
     return nf;
 }
 
-// Nearest fresh item that passes the current bound (wave argmin over fd[0 .. nf)); +inf if none.
-__device__ __forceinline__ float nearest_fresh(const float *fd, int nf, int &bf)
+// VisitedTable reset list: this hop's fresh ids, appended once the hop's bookkeeping is done, so the
+// stores' acknowledgements overlap the next hop's row load and visited atomics (which wait on vmcnt
+// anyway) instead of stalling this hop's distance loads.
+__device__ __forceinline__ int append_clear(const FlatArgs &a, int32_t *clr, int clear_n, const uint32_t *fid, int nf)
 {
-    const int lane = lane_id_local();
-    float bd = INFINITY;
-    bf = 0x7FFFFFFF;
-    for (int f = lane; f < nf; f += 64) {
-        const float d = fd[f];
-        if (d < bd) {
-            bd = d;
-            bf = f;
-        }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float od = __shfl_xor(bd, off);
-        const int of = __shfl_xor(bf, off);
-        if (od < bd || (od == bd && of < bf)) {
-            bd = od;
-            bf = of;
-        }
-    }
-    bf = __builtin_amdgcn_readfirstlane(bf);
-    return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(bd)));
+    for (int f = lane_id_local(); f < nf; f += 64)
+        if (clear_n + f < a.clear_cap)
+            clr[clear_n + f] = (int32_t)fid[f];
+    return clear_n + nf;
 }
 
 __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
@@ -435,19 +486,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
     uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     float *q = reinterpret_cast<float *>(smem);                      // [d]
-    float *topk = q + a.d;                                           // [top_lds]
-    uint32_t *topi = reinterpret_cast<uint32_t *>(topk + a.top_lds); // [top_lds]
-    float *cdk = reinterpret_cast<float *>(topi + a.top_lds);        // [cand_lds]
-    uint32_t *cdi = reinterpret_cast<uint32_t *>(cdk + a.cand_lds); // [cand_lds]
-    uint32_t *fid = cdi + a.cand_lds;                               // [maxM0] fresh ids / upper links
+    KV *topkv = reinterpret_cast<KV *>(q + a.d);                    // [top_lds] (d % 16 == 0: aligned)
+    KV *cdkv = topkv + a.top_lds;                                   // [cand_lds]
+    uint32_t *fid = reinterpret_cast<uint32_t *>(cdkv + a.cand_lds); // [maxM0] fresh ids / upper links
     float *fd = reinterpret_cast<float *>(fid + a.maxM0);           // [maxM0] their distances
     int *sh = reinterpret_cast<int *>(fd + a.maxM0);                // [4] broadcast scalars
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
-    const HeapRef<true> top{topk, topi, a.top_lds, a.top_ovf_k + (size_t)blockIdx.x * (size_t)a.top_ovf_cap,
-                            a.top_ovf_i + (size_t)blockIdx.x * (size_t)a.top_ovf_cap};
-    const HeapRef<true> cand{cdk, cdi, a.cand_lds, a.cand_ovf_k + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap,
-                             a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap};
+    const HeapRef<true> top{(DRM_LDS uint64_t *)topkv, a.top_lds,
+                            (DRM_GLOBAL float *)(a.top_ovf_k + (size_t)blockIdx.x * (size_t)a.top_ovf_cap),
+                            (DRM_GLOBAL uint32_t *)(a.top_ovf_i + (size_t)blockIdx.x * (size_t)a.top_ovf_cap)};
+    const HeapRef<true> cand{(DRM_LDS uint64_t *)cdkv, a.cand_lds,
+                             (DRM_GLOBAL float *)(a.cand_ovf_k + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap),
+                             (DRM_GLOBAL uint32_t *)(a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap)};
     const int cand_cap = a.cand_lds + (int)a.cand_ovf_cap;
     // queue: 0 .. n-1, or (fallback pass) the *qcount query ids in qlist
     const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
@@ -528,10 +579,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
             if (a.clear_cap > 0)
                 clr[0] = (int32_t)cur;
         }
-        // row of the predicted next candidate, loaded during the bookkeeping of this hop (maxM0 <= 128)
-        uint32_t pf_c = ~0u, pf_w0 = 0u, pf_w1 = 0u;
-        int pf_cnt = 0;
-        const bool narrow = a.maxM0 <= 128;
         bool keep = true; // false: handed to the exact pass (NR > 0)
         int nres = 0;
         if constexpr (NR > 0) {
@@ -578,42 +625,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                     }
                 nhops++;
                 FLAT_STAMP(1); // next candidate
-                const int nf = expand_row(a, c, vis, clr, clear_n, fid, c == pf_c, pf_cnt, pf_w0, pf_w1);
-                clear_n += nf;
+                const int nf = expand_row(a, c, vis, fid, false, 0u, 0u);
                 FLAT_STAMP(2); // row + visited
                 l2_dispatch<NV>(a, q, qr, fid, nf, fd);
                 ndis += nf;
                 FLAT_STAMP(3); // distances
-                if (narrow) { // next expansion: the first unexpanded entry, or a nearer accepted link
-                    int bf;
-                    const float bd = nearest_fresh(fd, nf, bf);
-                    int e2 = -1;
-#pragma unroll
-                    for (int r = 0; r < NR; ++r) {
-                        const uint64_t m = __ballot(64 * r + lane < tsz && !(ti[r] >> 31));
-                        if (e2 < 0 && m)
-                            e2 = 64 * r + __builtin_ctzll(m);
-                    }
-                    float ek = INFINITY;
-                    uint32_t eid = ~0u;
-#pragma unroll
-                    for (int r = 0; r < NR; ++r)
-                        if (e2 >= 0 && (e2 >> 6) == r) {
-                            ek = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(tk[r]), e2 & 63));
-                            eid = __builtin_amdgcn_readlane(ti[r], e2 & 63);
-                        }
-                    uint32_t pred = eid;
-                    if (bf < nf && (tsz < a.ef || bd < lb) && bd < ek)
-                        pred = fid[bf];
-                    pred = __builtin_amdgcn_readfirstlane(pred);
-                    if (pred != ~0u && pred != pf_c) {
-                        const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
-                        pf_c = pred;
-                        pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
-                        pf_w0 = prow[min(lane, a.maxM0 - 1)];
-                        pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
-                    }
-                }
                 // consideration in link order: insert each accepted link by rank
                 for (int base = 0; base < nf && keep; base += 64) {
                     const int f = base + lane;
@@ -666,6 +682,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                                 lb = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(tk[r]), (tsz - 1) & 63));
                     }
                 }
+                clear_n = append_clear(a, clr, clear_n, fid, nf);
                 __syncthreads();
                 FLAT_STAMP(4); // consideration
                 if (!keep)
@@ -696,110 +713,111 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
             __syncthreads();
             FLAT_STAMP(0); // query setup + upper levels
             const bool top_par = a.ef + 1 <= min(a.top_lds, 513); // top_candidates in LDS, parallel ops
-            while (cand_len > 0) {
-                const float cdist = -cand.key(0);
+            // Fast hop loop: both heaps entirely in LDS, wave-parallel heap ops, no global access but
+            // the row / visited / distance / prefetch traffic itself. The first link that would take
+            // candidate_set past its LDS part ends it; the query then finishes in the slow loop below
+            // (also taken from the start when top_candidates does not fit). Keeping the serial
+            // replay's global accesses out of this loop keeps its waits off the row prefetch.
+            bool slow = !top_par;
+            int slow_base = -1, slow_nf = 0;
+            uint64_t slow_mask = 0;
+            while (!slow && cand_len > 0) {
+                const float cdist = -kv_key(cdkv[0]); // slot 0 is always in LDS
                 if (cdist > lowerBound)
                     break;
-                const uint32_t c = cand.id(0);
+                const uint32_t c = cdkv[0].y;
+                // the row loads go out before the pop, which then overlaps their latency
+                const uint32_t *crow = a.l0 + (size_t)c * (size_t)a.maxM0;
+                const uint32_t w0 = lane < a.maxM0 ? crow[lane] : ~0u;
+                const uint32_t w1 = 64 + lane < a.maxM0 ? crow[64 + lane] : ~0u;
                 __syncthreads();
-                if (cand_len > 1) {
-                    if (cand_len <= a.cand_lds) {
-                        par_pop_any(cdk, cdi, cand_len);
-                    } else {
-                        if (lane == 0)
-                            stl_pop(cand, cand_len);
-                        __syncthreads();
-                    }
-                }
+                if (cand_len > 1)
+                    par_pop_any(cdkv, cand_len);
                 cand_len--;
                 nhops++;
                 FLAT_STAMP(1); // candidate_set pop
-                const int nf = expand_row(a, c, vis, clr, clear_n, fid, c == pf_c, pf_cnt, pf_w0, pf_w1);
-                clear_n += nf;
+                const int nf = expand_row(a, c, vis, fid, true, w0, w1);
                 FLAT_STAMP(2); // row + visited
                 l2_dispatch<NV>(a, q, qr, fid, nf, fd);
                 ndis += nf;
                 FLAT_STAMP(3); // distances
-                if (narrow) { // next pop: the candidate_set root, or a nearer link passing the bound
-                    int bf;
-                    const float bd = nearest_fresh(fd, nf, bf);
-                    const float croot = cand_len > 0 ? -cand.key(0) : INFINITY;
-                    uint32_t pred = ~0u;
-                    if (bf < nf && (top_len < a.ef || bd < lowerBound) && bd < croot)
-                        pred = fid[bf];
-                    else if (cand_len > 0)
-                        pred = cand.id(0);
-                    pred = __builtin_amdgcn_readfirstlane(pred);
-                    if (pred != ~0u && pred != pf_c) {
-                        const uint32_t *prow = a.l0 + (size_t)pred * (size_t)a.maxM0;
-                        pf_c = pred;
-                        pf_cnt = (int)(a.l0cnt[pred] & 0xFFFFu);
-                        pf_w0 = prow[min(lane, a.maxM0 - 1)];
-                        pf_w1 = prow[min(64 + lane, a.maxM0 - 1)];
-                    }
-                }
                 // consideration in link order: `if (top.size() < ef || lowerBound > dist)` push both
                 // heaps, trim top to ef. lowerBound only falls once top is full, so one ballot per 64
                 // links picks a superset of the accepted ones (the exact test is rechecked).
-                for (int base = 0; base < nf; base += 64) {
+                for (int base = 0; base < nf && !slow; base += 64) {
                     const int f = base + lane;
                     const float dl = f < nf ? fd[f] : INFINITY;
                     const uint32_t il = f < nf ? fid[f] : 0u;
                     uint64_t mask = __ballot(f < nf && (top_len < a.ef || lowerBound > dl));
                     while (mask) {
                         const int b = __builtin_ctzll(mask);
-                        mask &= mask - 1;
                         const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
-                        if (!(top_len < a.ef || lowerBound > dist))
+                        if (!(top_len < a.ef || lowerBound > dist)) {
+                            mask &= mask - 1;
                             continue;
-                        if (cand_len >= cand_cap) {
-                            overflow = true;
+                        }
+                        if (cand_len + 1 > a.cand_lds) { // hand the rest of this hop to the slow loop
+                            slow = true;
+                            slow_base = base;
+                            slow_mask = mask;
+                            slow_nf = nf;
                             break;
                         }
+                        mask &= mask - 1;
                         const uint32_t id = __builtin_amdgcn_readlane(il, b);
-                        if (++cand_len <= a.cand_lds) {
-                            par_push(cdk, cdi, cand_len, -dist, id);
-                        } else {
-                            if (lane == 0) {
-                                cand.set(cand_len - 1, -dist, id);
-                                stl_push(cand, cand_len, -dist, id);
-                            }
-                            __syncthreads();
-                        }
-                        ++top_len;
-                        if (top_par) {
-                            if (par_push(topk, topi, top_len, dist, id))
-                                lowerBound = dist;
-                            while (top_len > a.ef)
-                                lowerBound = par_pop_any(topk, topi, top_len--);
-                        } else {
-                            if (lane == 0) {
-                                top.set(top_len - 1, dist, id);
-                                stl_push(top, top_len, dist, id);
-                                int tl = top_len;
-                                while (tl > a.ef)
-                                    stl_pop(top, tl--);
-                                sh[2] = __float_as_int(top.key(0));
-                            }
-                            __syncthreads();
-                            top_len = min(top_len, a.ef);
-                            lowerBound = __int_as_float(sh[2]);
-                        }
+                        par_push(cdkv, ++cand_len, -dist, id);
+                        if (par_push(topkv, ++top_len, dist, id))
+                            lowerBound = dist;
+                        while (top_len > a.ef)
+                            lowerBound = par_pop_any(topkv, top_len--);
                     }
-                    if (overflow)
-                        break;
                 }
+                clear_n = append_clear(a, clr, clear_n, fid, nf);
                 __syncthreads();
                 FLAT_STAMP(4); // consideration: heap pushes / pops
-                if (overflow)
-                    break;
+            }
+            if (slow) {
+                ConsState st{top_len, cand_len, lowerBound, 0};
+                if (slow_base >= 0) { // the rest of the interrupted hop (its fresh links are still in LDS)
+                    st = slow_consider(fd, fid, slow_nf, slow_base, slow_mask, st, top, cand, topkv, cdkv, a.ef,
+                                       a.cand_lds, cand_cap, top_par, sh);
+                    clear_n = append_clear(a, clr, clear_n, fid, slow_nf);
+                }
+                while (!st.overflow && st.cand_len > 0) {
+                    const float cdist = -cand.key(0);
+                    if (cdist > st.lb)
+                        break;
+                    const uint32_t c = cand.id(0);
+                    __syncthreads();
+                    if (st.cand_len > 1) {
+                        if (st.cand_len <= a.cand_lds)
+                            par_pop_any(cdkv, st.cand_len);
+                        else
+                            serial_cand_pop(cand, st.cand_len);
+                    }
+                    st.cand_len--;
+                    nhops++;
+                    const int nf = expand_row(a, c, vis, fid, false, 0u, 0u);
+                    l2_dispatch<NV>(a, q, qr, fid, nf, fd);
+                    ndis += nf;
+                    const int f = lane;
+                    const float dl = f < nf ? fd[f] : INFINITY;
+                    st = slow_consider(fd, fid, nf, 0, __ballot(f < nf && (st.top_len < a.ef || st.lb > dl)), st, top,
+                                       cand, topkv, cdkv, a.ef, a.cand_lds, cand_cap, top_par, sh);
+                    clear_n = append_clear(a, clr, clear_n, fid, nf);
+                    __syncthreads();
+                }
+                top_len = st.top_len;
+                cand_len = st.cand_len;
+                lowerBound = st.lb;
+                overflow = st.overflow != 0;
             }
             if (lane == 0 && overflow)
                 atomicAdd(a.counter + 1, 1u); // candidate_set overflow: reported by the host entry points
             // --- while (top.size() > k) top.pop(); then order survivors by (dist, label)
             if (top_par) {
                 while (top_len > a.k)
-                    par_pop_any(topk, topi, top_len--);
+                    par_pop_any(topkv, top_len--);
             } else {
                 if (lane == 0) {
                     int tl = top_len;
@@ -812,7 +830,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
             nres = top_len;
             // searchKnnCloserFirst order: ascending (dist, label) -- rank by counting, labels staged
             // in the (now idle) candidate-heap LDS when they fit
-            uint64_t *lab = reinterpret_cast<uint64_t *>(cdk);
+            uint64_t *lab = reinterpret_cast<uint64_t *>(cdkv);
             const bool staged = nres <= a.cand_lds;
             if (staged)
                 for (int e = lane; e < nres; e += 64)
