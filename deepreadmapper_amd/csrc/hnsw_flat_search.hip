@@ -122,6 +122,9 @@ template <bool OVF> __device__ void stl_pop(const HeapRef<OVF> &h, int len)
 // ---- wave-parallel versions of the same two heap operations, for a heap held entirely in LDS.
 // They leave exactly the layout the serial replay above leaves (so every later tie resolves the same
 // way), but cost one LDS round trip plus a few ballots instead of one dependent LDS access per level.
+// ballot of a bool straight from its compare mask (HIP's int __ballot adds a select + compare)
+__device__ __forceinline__ uint64_t bal(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
 __device__ __forceinline__ int heap_depth(int slot) { return 31 - __builtin_clz((unsigned)slot + 1u); }
 
 // __push_heap for the element just appended at slot len-1. Along the ancestor chain keys only grow
@@ -138,7 +141,7 @@ __device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
     const int anc = valid ? ((hole + 1) >> j) - 1 : 0;
     const KV ae = H[anc];
     const bool lt = valid && kv_key(ae) < vk;
-    const int h = __popcll(__ballot(lt));
+    const int h = __popcll(bal(lt));
     if (lt) // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
         H[((hole + 1) >> (j - 1)) - 1] = ae;
     if (lane == 0)
@@ -150,56 +153,60 @@ __device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
 // element): the hole walks from the root to a leaf along the larger child (ties -> right child, a
 // lone left child taken), then the old last element v sifts back up that same path. Net effect on
 // the path P_0 = root .. P_m = leaf: with h = #{i >= 1 : key(P_i) < v}, P_0 .. P_{m-h-1} each take
-// their successor's entry, P_{m-h} takes v, the rest stay. Lanes own nodes p = lane + 64 jj and hold
-// both children of p, so the child choices are one ballot per 64 nodes; the leaf is found by a scalar
-// walk over those bits. NN = node groups (L <= 128 NN + 1). Children are read without a bounds
-// select: slots up to 128 NN stay inside the wave's LDS (the heap regions are followed by others) and
-// entries past L never take part. Returns the new root key.
+// their successor's entry, P_{m-h} takes v, the rest stay (keys along the path only fall, so those
+// P_i are a suffix). Lanes own nodes p = lane + 64 jj and read both children of p, so the child
+// choices are one ballot per 64 nodes; the leaf is found by a scalar walk over those bits (heap_walk);
+// then lane i reads P_{i+1} (the entry that moves up into P_i), one ballot gives h, one write phase.
+// NN = node groups (L <= 128 NN + 1). Children are read without a bounds select: slots up to 128 NN
+// stay inside the wave's LDS (the heap regions are followed by others) and entries past L never take
+// part. Returns the new root key.
+template <int NN> __device__ __forceinline__ int heap_walk(const uint64_t (&bits)[NN], int L)
+{
+    // u = node + 1; node u - 1 has a child iff 2u <= L. Nodes 0 .. 63 are all in bits[0].
+    int u = 1;
+#pragma unroll
+    for (int d = 0; d < 7; ++d)
+        if (2 * u <= L && (NN == 1 || u <= 64))
+            u = 2 * u + (int)((bits[0] >> (u - 1)) & 1ull);
+    if constexpr (NN > 1) {
+        while (2 * u <= L) {
+            const int p = u - 1;
+            uint64_t mk = bits[0];
+#pragma unroll
+            for (int jj = 1; jj < NN; ++jj)
+                if ((p >> 6) == jj)
+                    mk = bits[jj];
+            u = 2 * u + (int)((mk >> (p & 63)) & 1ull);
+        }
+    }
+    return u - 1;
+}
+
 template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
 {
     const int lane = lane_id_local();
     const int L = len - 1;
     const KV ve = H[L];
     const float vk = kv_key(ve);
-    KV ce[NN];
     uint64_t bits[NN];
 #pragma unroll
     for (int jj = 0; jj < NN; ++jj) {
         const int p = lane + 64 * jj;
         const KV le = H[2 * p + 1], re = H[2 * p + 2];
-        const bool right = 2 * p + 2 < L && !(kv_key(re) < kv_key(le));
-        ce[jj] = right ? re : le;
-        bits[jj] = __ballot(right);
+        bits[jj] = bal((2 * p + 2 < L) & !(kv_key(re) < kv_key(le)));
     }
-    int leaf = 0;
-    while (2 * leaf + 1 < L) {
-        uint64_t mk = bits[0];
-#pragma unroll
-        for (int jj = 1; jj < NN; ++jj)
-            if ((leaf >> 6) == jj)
-                mk = bits[jj];
-        leaf = 2 * leaf + 1 + (int)((mk >> (leaf & 63)) & 1ull);
-    }
+    const int leaf = heap_walk<NN>(bits, L);
     const int m = heap_depth(leaf);
-    int h = 0;
-    bool on[NN];
-#pragma unroll
-    for (int jj = 0; jj < NN; ++jj) {
-        const int p = lane + 64 * jj;
-        const int dp = heap_depth(p);
-        on[jj] = dp < m && (((leaf + 1) >> (m - dp)) == p + 1);
-        h += __popcll(__ballot(on[jj] && kv_key(ce[jj]) < vk));
-    }
+    const int j = lane + 1;
+    const bool valid = j <= m;
+    const KV ce = H[valid ? ((leaf + 1) >> (m - j)) - 1 : 0]; // P_{lane + 1}
+    const int h = __popcll(bal(valid & (kv_key(ce) < vk)));
     const int t = m - h; // depth where v lands
-#pragma unroll
-    for (int jj = 0; jj < NN; ++jj) {
-        const int p = lane + 64 * jj;
-        if (on[jj] && heap_depth(p) < t)
-            H[p] = ce[jj];
-    }
+    if (lane < t)
+        H[((leaf + 1) >> (m - lane)) - 1] = ce;
     if (lane == 0)
         H[((leaf + 1) >> h) - 1] = ve;
-    return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(ce[0].x, 0)) : vk;
+    return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(ce.x, 0)) : vk;
 }
 
 // heaps of up to 513 entries (the callers take the serial replay beyond)
@@ -353,7 +360,7 @@ __device__ __forceinline__ ConsState slow_consider(const float *fd, const uint32
         const int f = base + lane;
         const float dl = f < nf ? fd[f] : INFINITY;
         const uint32_t il = f < nf ? fid[f] : 0u;
-        uint64_t mask = base == base0 ? mask0 : __ballot(f < nf && (st.top_len < ef || st.lb > dl));
+        uint64_t mask = base == base0 ? mask0 : bal(f < nf && (st.top_len < ef || st.lb > dl));
         while (mask) {
             const int b = __builtin_ctzll(mask);
             mask &= mask - 1;
@@ -437,7 +444,7 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
                 fresh1 = fresh1 && !(jj < j1 && vj == v1);
             }
         }
-        const uint64_t fm0 = __ballot(fresh0), fm1 = __ballot(fresh1);
+        const uint64_t fm0 = bal(fresh0), fm1 = bal(fresh1);
         const int n0 = __popcll(fm0);
         if (fresh0)
             fid[nf + __popcll(fm0 & below)] = v0;
@@ -609,7 +616,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                 int e = -1;
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    const uint64_t m = __ballot(64 * r + lane < tsz && !(ti[r] >> 31));
+                    const uint64_t m = bal(64 * r + lane < tsz && !(ti[r] >> 31));
                     if (e < 0 && m)
                         e = 64 * r + __builtin_ctzll(m);
                 }
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                     const int f = base + lane;
                     const float dl = f < nf ? fd[f] : INFINITY;
                     const uint32_t il = f < nf ? fid[f] : 0u;
-                    uint64_t mask = __ballot(f < nf && (tsz < a.ef || lb > dl));
+                    uint64_t mask = bal(f < nf && (tsz < a.ef || lb > dl));
                     while (mask) {
                         const int b = __builtin_ctzll(mask);
                         mask &= mask - 1;
@@ -648,8 +655,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
 #pragma unroll
                         for (int r = 0; r < NR; ++r) {
                             const bool valid = 64 * r + lane < tsz;
-                            rank += __popcll(__ballot(valid && tk[r] < dist));
-                            eq |= __ballot(valid && tk[r] == dist);
+                            rank += __popcll(bal(valid && tk[r] < dist));
+                            eq |= bal(valid && tk[r] == dist);
                         }
                         if (eq) {
                             keep = false;
@@ -748,7 +755,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                     const int f = base + lane;
                     const float dl = f < nf ? fd[f] : INFINITY;
                     const uint32_t il = f < nf ? fid[f] : 0u;
-                    uint64_t mask = __ballot(f < nf && (top_len < a.ef || lowerBound > dl));
+                    uint64_t mask = bal(f < nf && (top_len < a.ef || lowerBound > dl));
                     while (mask) {
                         const int b = __builtin_ctzll(mask);
                         const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                     ndis += nf;
                     const int f = lane;
                     const float dl = f < nf ? fd[f] : INFINITY;
-                    st = slow_consider(fd, fid, nf, 0, __ballot(f < nf && (st.top_len < a.ef || st.lb > dl)), st, top,
+                    st = slow_consider(fd, fid, nf, 0, bal(f < nf && (st.top_len < a.ef || st.lb > dl)), st, top,
                                        cand, topkv, cdkv, a.ef, a.cand_lds, cand_cap, top_par, sh);
                     clear_n = append_clear(a, clr, clear_n, fid, nf);
                     __syncthreads();

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Builds an alternate libdrm_hip.so with extra -D flags on the HIP kernels, for A/B timing on one box
+# (tools/scripts/ab.sh, DRM_LIB). Usage: bash tools/scripts/build_variant.sh NAME [-DFLAG=V ...]
+# -> ab/NAME.so (git-ignored; travels to the GPU box with the tree). Run `make` first.
+set -e
+NAME=$1; shift
+ROCM=${ROCM:-/opt/rocm}
+mkdir -p ab/$NAME.obj
+FL="-O3 -std=c++17 -fPIC -Iinclude -Ideepreadmapper_amd/csrc -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off -munsafe-fp-atomics $*"
+for k in hnsw_search hnsw_search_lds hnsw_flat_search sw_rerank; do
+  $ROCM/bin/hipcc $FL -c deepreadmapper_amd/csrc/$k.hip -o ab/$NAME.obj/$k.o &
+done
+wait
+$ROCM/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$NAME.so ab/$NAME.obj/*.o build/capi.o build/faiss_io.o \
+  build/formats.o build/builder.o build/embed.o build/hnswlib_io.o build/builder_flat.o -L$ROCM/lib -lamdhip64 -lgomp \
+  -Wl,-soname,libdrm_hip.so
+echo ab/$NAME.so
