@@ -415,8 +415,8 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
     const uint32_t *row = a.l0 + (size_t)c * (size_t)a.maxM0;
     uint32_t r0, r1;
     if (have_pf) {
-        r0 = pf_w0;
-        r1 = pf_w1;
+        r0 = lane < a.maxM0 ? pf_w0 : ~0u; // the loads were clamped to the row (see the hop loop)
+        r1 = 64 + lane < a.maxM0 ? pf_w1 : ~0u;
     } else {
         r0 = lane < a.maxM0 ? row[lane] : ~0u;
         r1 = 64 + lane < a.maxM0 ? row[64 + lane] : ~0u;
@@ -735,8 +735,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                 const uint32_t c = cdkv[0].y;
                 // the row loads go out before the pop, which then overlaps their latency
                 const uint32_t *crow = a.l0 + (size_t)c * (size_t)a.maxM0;
-                const uint32_t w0 = lane < a.maxM0 ? crow[lane] : ~0u;
-                const uint32_t w1 = 64 + lane < a.maxM0 ? crow[64 + lane] : ~0u;
+                // unconditional (clamped) loads, masked when used: no register init that would wait
+                // for the VMEM counter to drain first
+                const uint32_t w0 = crow[min(lane, a.maxM0 - 1)];
+                const uint32_t w1 = crow[min(64 + lane, a.maxM0 - 1)];
                 __syncthreads();
                 if (cand_len > 1)
                     par_pop_any(cdkv, cand_len);
