@@ -43,6 +43,15 @@ __device__ __forceinline__ int lane_id_local()
 typedef uint2 KV;
 __device__ __forceinline__ float kv_key(KV e) { return __uint_as_float(e.x); }
 __device__ __forceinline__ KV kv_make(float k, uint32_t i) { return make_uint2(__float_as_uint(k), i); }
+// One 8-byte LDS read whose both halves are live right away. Left alone, the compiler reads the key,
+// waits, and fetches the id later only in the lanes that move it -- a second dependent LDS round
+// trip in every heap operation.
+__device__ __forceinline__ KV kv_load(const KV *p)
+{
+    KV e = *p;
+    asm volatile("" : "+v"(e.x), "+v"(e.y));
+    return e;
+}
 
 // Address-space-qualified pointers: an access that may go to either part stays a branch between an
 // LDS and a global instruction. Generic pointers would let the compiler fold the two into one flat_*
@@ -139,7 +148,7 @@ __device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
     const int j = lane + 1;
     const bool valid = j <= m;
     const int anc = valid ? ((hole + 1) >> j) - 1 : 0;
-    const KV ae = H[anc];
+    const KV ae = kv_load(H + anc);
     const bool lt = valid && kv_key(ae) < vk;
     const int h = __popcll(bal(lt));
     if (lt) // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
@@ -147,6 +156,34 @@ __device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
     if (lane == 0)
         H[((hole + 1) >> h) - 1] = kv_make(vk, vi);
     return h == m;
+}
+
+// candidate_set.emplace(-dist, id) then top_candidates.emplace(dist, id) (par_push twice): the two
+// heaps are disjoint, so both ancestor reads go out in one LDS round trip. Returns true when dist
+// became top_candidates' root.
+__device__ __forceinline__ bool par_push2(KV *Cd, int clen, KV *T, int tlen, float dist, uint32_t id)
+{
+    const int lane = lane_id_local();
+    const int j = lane + 1;
+    const int chole = clen - 1, cm = heap_depth(chole);
+    const int thole = tlen - 1, tm = heap_depth(thole);
+    const bool cvalid = j <= cm, tvalid = j <= tm;
+    KV ca = Cd[cvalid ? ((chole + 1) >> j) - 1 : 0];
+    KV ta = T[tvalid ? ((thole + 1) >> j) - 1 : 0];
+    asm volatile("" : "+v"(ca.x), "+v"(ca.y), "+v"(ta.x), "+v"(ta.y));
+    const bool clt = cvalid && kv_key(ca) < -dist;
+    const int hc = __popcll(bal(clt));
+    if (clt)
+        Cd[((chole + 1) >> (j - 1)) - 1] = ca;
+    if (lane == 0)
+        Cd[((chole + 1) >> hc) - 1] = kv_make(-dist, id);
+    const bool tlt = tvalid && kv_key(ta) < dist;
+    const int ht = __popcll(bal(tlt));
+    if (tlt)
+        T[((thole + 1) >> (j - 1)) - 1] = ta;
+    if (lane == 0)
+        T[((thole + 1) >> ht) - 1] = kv_make(dist, id);
+    return ht == tm;
 }
 
 // pop_heap + pop_back for len > 1 (libstdc++ __adjust_heap then __push_heap of the old last
@@ -186,8 +223,8 @@ template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
 {
     const int lane = lane_id_local();
     const int L = len - 1;
-    const KV ve = H[L];
-    const float vk = kv_key(ve);
+    const KV ve = kv_load(H + L);
+    const float vk = __uint_as_float(__builtin_amdgcn_readfirstlane(ve.x)); // uniform (ve is opaque)
     uint64_t bits[NN];
 #pragma unroll
     for (int jj = 0; jj < NN; ++jj) {
@@ -199,7 +236,7 @@ template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
     const int m = heap_depth(leaf);
     const int j = lane + 1;
     const bool valid = j <= m;
-    const KV ce = H[valid ? ((leaf + 1) >> (m - j)) - 1 : 0]; // P_{lane + 1}
+    const KV ce = kv_load(H + (valid ? ((leaf + 1) >> (m - j)) - 1 : 0)); // P_{lane + 1}
     const int h = __popcll(bal(valid & (kv_key(ce) < vk)));
     const int t = m - h; // depth where v lands
     if (lane < t)
@@ -257,6 +294,9 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 // Same distances with the query slice in registers (qr[r] = q[sub + 8r], NV = d / 8 per lane) and
 // every load of a pass issued before the first use: 16 items per pass, two per lane group, so a
 // hop's distances cost one memory round trip instead of one per dimension step.
+#ifndef DRM_FLAT_PUSH2
+#define DRM_FLAT_PUSH2 1 // 1: both pushes of an accepted link share one LDS round trip (par_push2)
+#endif
 #ifndef DRM_FLAT_TWO_SETS
 #define DRM_FLAT_TWO_SETS 0 // 1: 16 items per pass (two per lane group); 0: 8 (fewer VGPRs)
 #endif
@@ -729,10 +769,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
             int slow_base = -1, slow_nf = 0;
             uint64_t slow_mask = 0;
             while (!slow && cand_len > 0) {
-                const float cdist = -kv_key(cdkv[0]); // slot 0 is always in LDS
+                const KV croot = kv_load(cdkv); // slot 0 is always in LDS
+                const float cdist = -__uint_as_float(__builtin_amdgcn_readfirstlane(croot.x));
                 if (cdist > lowerBound)
                     break;
-                const uint32_t c = cdkv[0].y;
+                const uint32_t c = __builtin_amdgcn_readfirstlane(croot.y);
                 // the row loads go out before the pop, which then overlaps their latency
                 const uint32_t *crow = a.l0 + (size_t)c * (size_t)a.maxM0;
                 // unconditional (clamped) loads, masked when used: no register init that would wait
@@ -774,9 +815,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hn
                         }
                         mask &= mask - 1;
                         const uint32_t id = __builtin_amdgcn_readlane(il, b);
+#if DRM_FLAT_PUSH2
+                        if (par_push2(cdkv, ++cand_len, topkv, ++top_len, dist, id))
+                            lowerBound = dist;
+#else
                         par_push(cdkv, ++cand_len, -dist, id);
                         if (par_push(topkv, ++top_len, dist, id))
                             lowerBound = dist;
+#endif
                         while (top_len > a.ef)
                             lowerBound = par_pop_any(topkv, top_len--);
                     }
