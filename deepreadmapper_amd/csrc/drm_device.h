@@ -98,7 +98,7 @@ struct DeviceFlatIndex {
     uint32_t ep = 0;
     int64_t ntotal = 0;
     int32_t has_dup_links = 0;
-    int32_t waves_per_cu = 24;  // resident search waves per CU (6 per SIMD at <= 80 VGPRs)
+    int32_t waves_per_cu = 32;  // cap on resident search waves per CU (the kernel build sets the real one)
     int32_t try_sorted = 0;    // DRM_SEARCH_SORTED=1: tie-free sorted-array pass first, exact pass after
     float *vec = nullptr;      // [ntotal][d] f32 (512-B rows at d = 128)
     uint32_t *l0 = nullptr;    // [ntotal][maxM0] level-0 links (512-B rows at maxM0 = 128)

@@ -294,6 +294,12 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 // Same distances with the query slice in registers (qr[r] = q[sub + 8r], NV = d / 8 per lane) and
 // every load of a pass issued before the first use: 16 items per pass, two per lane group, so a
 // hop's distances cost one memory round trip instead of one per dimension step.
+#ifndef DRM_FLAT_WAVES
+#define DRM_FLAT_WAVES 8 // resident waves per SIMD the kernel is register-budgeted for (4x per CU)
+#endif
+#ifndef DRM_FLAT_CAND_LDS
+#define DRM_FLAT_CAND_LDS 376 // candidate_set entries in LDS (5 KB per wave at 8 waves/SIMD); ~2 % of C3 queries outgrow it and finish in the slow loop
+#endif
 #ifndef DRM_FLAT_PUSH2
 #define DRM_FLAT_PUSH2 1 // 1: both pushes of an accepted link share one LDS round trip (par_push2)
 #endif
@@ -526,14 +532,15 @@ __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
 // NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
 // NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
 template <int NV, int NR, bool STAMPS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void hnsw_flat_search_kernel(FlatArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAVES))) void hnsw_flat_search_kernel(FlatArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
     uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    float *q = reinterpret_cast<float *>(smem);                      // [d]
-    KV *topkv = reinterpret_cast<KV *>(q + a.d);                    // [top_lds] (d % 16 == 0: aligned)
+    constexpr bool q_lds = NV == 0 || !DRM_FLAT_Q_REGS;               // query slice in registers otherwise
+    float *q = reinterpret_cast<float *>(smem);                      // [d] (q_lds)
+    KV *topkv = reinterpret_cast<KV *>(q + (q_lds ? a.d : 0));      // [top_lds] (d % 16 == 0: aligned)
     KV *cdkv = topkv + a.top_lds;                                   // [cand_lds]
     uint32_t *fid = reinterpret_cast<uint32_t *>(cdkv + a.cand_lds); // [maxM0] fresh ids / upper links
     float *fd = reinterpret_cast<float *>(fid + a.maxM0);           // [maxM0] their distances
@@ -948,14 +955,15 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         throw Error(DRM_ERR_UNSUPPORTED, "fp32 search needs d % 16 == 0 (hnswlib L2SqrSIMD16Ext)");
     int cus = 0;
     DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
-    const int cand_lds = 512;
+    const int cand_lds = DRM_FLAT_CAND_LDS;
     const int top_lds = std::min(efc + 1, 1024); // top_candidates beyond this continue in global memory
     const int64_t top_ovf = (int64_t)efc + 1 - top_lds;
-    const size_t lds = sizeof(float) * (size_t)ix.d + 8 * (size_t)top_lds + 8 * (size_t)cand_lds +
+    const bool q_lds = ix.d != 128 || !DRM_FLAT_Q_REGS; // the d = 128 kernel keeps the query in VGPRs
+    const size_t lds = sizeof(float) * (q_lds ? (size_t)ix.d : 0) + 8 * (size_t)top_lds + 8 * (size_t)cand_lds +
                        8 * (size_t)ix.maxM0 + 16;
     if (lds > 160 * 1024)
         throw Error(DRM_ERR_UNSUPPORTED, "fp32 search workspace does not fit in LDS (ef too large)");
-    const int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
+    const int per_cu = std::max(1, std::min(std::min(ix.waves_per_cu, 4 * DRM_FLAT_WAVES), (int)((160 * 1024) / lds)));
     const int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
     const int64_t words = (ix.ntotal + 31) / 32;
     const int64_t ovf_cap = 16384;
