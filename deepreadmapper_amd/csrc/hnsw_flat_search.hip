@@ -300,6 +300,9 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 #ifndef DRM_FLAT_CAND_LDS
 #define DRM_FLAT_CAND_LDS 376 // candidate_set entries in LDS (5 KB per wave at 8 waves/SIMD); ~2 % of C3 queries outgrow it and finish in the slow loop
 #endif
+#ifndef DRM_FLAT_VIS_LOAD
+#define DRM_FLAT_VIS_LOAD 1 // 1: visited test by L2 loads + marking of fresh links only; 0: returning atomicOr per link
+#endif
 #ifndef DRM_FLAT_PUSH2
 #define DRM_FLAT_PUSH2 1 // 1: both pushes of an accepted link share one LDS round trip (par_push2)
 #endif
@@ -477,10 +480,20 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
         const bool act0 = v0 != ~0u, act1 = v1 != ~0u;
         const uint32_t b0 = 1u << (v0 & 31), b1 = 1u << (v1 & 31);
         uint32_t o0 = ~0u, o1 = ~0u;
+#if DRM_FLAT_VIS_LOAD
+        // test with plain L2 loads, mark only the fresh links (non-returning atomics). The wave's
+        // earlier marks are all performed: VMEM completes in order and the row these ids came from
+        // was issued after them.
+        if (act0)
+            o0 = __hip_atomic_load(&vis[v0 >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (act1)
+            o1 = __hip_atomic_load(&vis[v1 >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
         if (act0)
             o0 = atomicOr(&vis[v0 >> 5], b0);
         if (act1)
             o1 = atomicOr(&vis[v1 >> 5], b1);
+#endif
         bool fresh0 = (o0 & b0) == 0u, fresh1 = (o1 & b1) == 0u;
         if (a.check_dups) { // a repeated link in one row: only its first occurrence is fresh
             const int cnt = (int)(a.l0cnt[c] & 0xFFFFu);
@@ -490,6 +503,12 @@ __device__ __forceinline__ int expand_row(const FlatArgs &a, uint32_t c, uint32_
                 fresh1 = fresh1 && !(jj < j1 && vj == v1);
             }
         }
+#if DRM_FLAT_VIS_LOAD
+        if (fresh0)
+            __hip_atomic_fetch_or(&vis[v0 >> 5], b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fresh1)
+            __hip_atomic_fetch_or(&vis[v1 >> 5], b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         const uint64_t fm0 = bal(fresh0), fm1 = bal(fresh1);
         const int n0 = __popcll(fm0);
         if (fresh0)
