@@ -537,6 +537,46 @@ __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false); // wave_shr:1
 }
 
+// Ascending (key, label) order of 128 pairs held as element i = lane + 64 r in register r: a bitonic
+// network, partners across lanes by ds_bpermute (j < 64) or within the lane (j = 64). Equal pairs
+// (only the +inf padding) may swap freely.
+__device__ __forceinline__ bool kl_less(float ka, uint64_t la, float kb, uint64_t lb)
+{
+    return ka < kb || (ka == kb && la < lb);
+}
+
+__device__ __forceinline__ void bitonic128(float (&k)[2], uint64_t (&l)[2])
+{
+    const int lane = lane_id_local();
+#pragma unroll
+    for (int kk = 2; kk <= 128; kk <<= 1) {
+#pragma unroll
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j == 64) { // kk == 128: ascending
+                if (kl_less(k[1], l[1], k[0], l[0])) {
+                    const float tk = k[0];
+                    const uint64_t tl = l[0];
+                    k[0] = k[1];
+                    l[0] = l[1];
+                    k[1] = tk;
+                    l[1] = tl;
+                }
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const float pk = __shfl_xor(k[r], j);
+                const uint64_t pl = __shfl_xor(l[r], j);
+                const bool lower = (lane & j) == 0;
+                const bool asc = ((lane + 64 * r) & kk) == 0;
+                const bool take = lower == asc ? kl_less(pk, pl, k[r], l[r]) : kl_less(k[r], l[r], pk, pl);
+                k[r] = take ? pk : k[r];
+                l[r] = take ? pl : l[r];
+            }
+        }
+    }
+}
+
 #define FLAT_STAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -909,25 +949,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
             }
             __syncthreads();
             nres = top_len;
-            // searchKnnCloserFirst order: ascending (dist, label) -- rank by counting, labels staged
-            // in the (now idle) candidate-heap LDS when they fit
-            uint64_t *lab = reinterpret_cast<uint64_t *>(cdkv);
-            const bool staged = nres <= a.cand_lds;
-            if (staged)
-                for (int e = lane; e < nres; e += 64)
-                    lab[e] = a.labels[top.id(e)];
-            __syncthreads();
-            for (int e = lane; e < nres; e += 64) {
-                const float de = top.key(e);
-                const uint64_t le = staged ? lab[e] : a.labels[top.id(e)];
-                int rank = 0;
-                for (int o = 0; o < nres; ++o) {
-                    const float dq = top.key(o);
-                    const uint64_t lo = staged ? lab[o] : a.labels[top.id(o)];
-                    rank += (dq < de) || (dq == de && lo < le);
+            // searchKnnCloserFirst order: ascending (dist, label)
+            if (top_par && nres <= 128) { // wave bitonic sort of the (at most 128) survivors
+                float sk[2];
+                uint64_t sl[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int e = lane + 64 * r;
+                    const bool v = e < nres;
+                    const KV te = topkv[v ? e : 0];
+                    sk[r] = v ? kv_key(te) : INFINITY;
+                    sl[r] = v ? a.labels[te.y] : ~0ull;
                 }
-                Dq[rank] = de;
-                Lq[rank] = le;
+                bitonic128(sk, sl);
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int e = lane + 64 * r;
+                    if (e < nres) {
+                        Dq[e] = sk[r];
+                        Lq[e] = sl[r];
+                    }
+                }
+            } else { // rank by counting, labels staged in the (now idle) candidate-heap LDS when they fit
+                uint64_t *lab = reinterpret_cast<uint64_t *>(cdkv);
+                const bool staged = nres <= a.cand_lds;
+                if (staged)
+                    for (int e = lane; e < nres; e += 64)
+                        lab[e] = a.labels[top.id(e)];
+                __syncthreads();
+                for (int e = lane; e < nres; e += 64) {
+                    const float de = top.key(e);
+                    const uint64_t le = staged ? lab[e] : a.labels[top.id(e)];
+                    int rank = 0;
+                    for (int o = 0; o < nres; ++o) {
+                        const float dq = top.key(o);
+                        const uint64_t lo = staged ? lab[o] : a.labels[top.id(o)];
+                        rank += (dq < de) || (dq == de && lo < le);
+                    }
+                    Dq[rank] = de;
+                    Lq[rank] = le;
+                }
             }
         }
         if (keep) {
@@ -943,14 +1004,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
             }
         }
         // VisitedTable reset: clear exactly the bits this query set
+        // (no wait for these stores: VMEM completes in order, so the next query's first visited test,
+        // which waits for loads issued after them, already sees them performed)
         if (clear_n <= a.clear_cap) {
+#pragma unroll 4
             for (int t = lane; t < clear_n; t += 64)
                 vis[(uint32_t)clr[t] >> 5] = 0u;
         } else {
             for (int64_t w = lane; w < a.vis_words; w += 64)
                 vis[w] = 0u;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         FLAT_STAMP(5); // result ordering + reset
     }
