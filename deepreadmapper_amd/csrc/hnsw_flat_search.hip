@@ -312,6 +312,11 @@ __device__ void l2_items(const FlatArgs &a, const float *q, const uint32_t *ids,
 #ifndef DRM_FLAT_Q_REGS
 #define DRM_FLAT_Q_REGS 1 // 1: the query slice stays in 16 VGPRs; 0: re-read from LDS per pass (occupancy)
 #endif
+#ifndef DRM_FLAT_PK
+#define DRM_FLAT_PK 0 // 1: packed-fp32 differences and squares (v_pk_add_f32 / v_pk_mul_f32): fewer
+                      // instructions but measured slower (12.8 vs 12.45 ms in one-box A/B), so off
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int NV>
 __device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float *q, const float (&qreg)[NV],
                                              const uint32_t *ids, int nitem, float *out)
@@ -336,11 +341,29 @@ __device__ __forceinline__ void l2_items_reg(const FlatArgs &a, const float *q, 
                 t1[r] = v1[8 * r];
         }
         float acc0 = 0.0f, acc1 = 0.0f;
+#if DRM_FLAT_PK
+        // dims r, r + 1 of the lane's accumulator: the differences and squares as v_pk_add_f32 /
+        // v_pk_mul_f32 (two IEEE ops per lane, the same roundings), the adds stay sequential
+#pragma unroll
+        for (int r = 0; r + 1 < NV; r += 2) {
+            const f32x2 qq = {qr[r], qr[r + 1]};
+            const f32x2 tt = {t0[r], t0[r + 1]};
+            const f32x2 df = qq - tt;
+            const f32x2 sq = df * df;
+            acc0 = __fadd_rn(acc0, sq.x);
+            acc0 = __fadd_rn(acc0, sq.y);
+        }
+        if (NV & 1) {
+            const float df = __fsub_rn(qr[NV - 1], t0[NV - 1]);
+            acc0 = __fadd_rn(acc0, __fmul_rn(df, df));
+        }
+#else
 #pragma unroll
         for (int r = 0; r < NV; ++r) {
             const float df = __fsub_rn(qr[r], t0[r]);
             acc0 = __fadd_rn(acc0, __fmul_rn(df, df));
         }
+#endif
         uint32_t p0 = __float_as_uint(acc0);
 #pragma unroll
         for (int s = 1; s < 8; ++s) {

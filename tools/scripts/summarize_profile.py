@@ -19,6 +19,19 @@ if os.path.exists(stats):
         out.append(f"{r['Name'][:90]:90s} calls={r['Calls']:>3s} avg_ms={float(r['AverageNs'])/1e6:9.3f} pct={float(r['Percentage']):6.2f}")
         js["kernels"].setdefault(r["Name"], {})["avg_ms"] = float(r["AverageNs"]) / 1e6
         js["kernels"][r["Name"]]["calls"] = int(r["Calls"])
+trace = os.path.join(d, "trace", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    # the first dispatch of each kernel is bench.py's warm-up (cold caches, first-touch bitmaps):
+    # the steady-state average over the rest is what bench.py's timed region compares with
+    durs = collections.defaultdict(list)
+    for r in csv.DictReader(open(trace)):
+        durs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    out.append("## steady-state dispatch durations (first dispatch = warm-up, excluded)")
+    for k, v in durs.items():
+        if len(v) > 1 and k in js["kernels"]:
+            js["kernels"][k]["avg_ms_steady"] = sum(v[1:]) / len(v[1:])
+            out.append(f"{k[:90]:90s} n={len(v) - 1:>3d} avg_ms={sum(v[1:]) / len(v[1:]):9.3f} "
+                       f"all=[{', '.join(f'{x:.3f}' for x in v)}]")
 out.append("## PMC (per dispatch averages)")
 for f in sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv"))):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
