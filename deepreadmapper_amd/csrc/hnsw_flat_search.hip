@@ -60,6 +60,10 @@ __device__ __forceinline__ KV kv_load(const KV *p)
 #define DRM_LDS __attribute__((address_space(3)))
 #define DRM_GLOBAL __attribute__((address_space(1)))
 
+#ifndef DRM_FLAT_MW
+#define DRM_FLAT_MW 1 // 1: heap ops write their moved entries and the new one in one write phase
+#endif
+
 // Heap array accessor: LDS part, plus (OVF) a per-slot global continuation past lds_cap entries.
 template <bool OVF> struct HeapRef {
     DRM_LDS uint64_t *kv;    // LDS entries [lds_cap], the KV pairs as (id << 32 | key bits)
@@ -151,10 +155,17 @@ __device__ __forceinline__ bool par_push(KV *H, int len, float vk, uint32_t vi)
     const KV ae = kv_load(H + anc);
     const bool lt = valid && kv_key(ae) < vk;
     const int h = __popcll(bal(lt));
+#if DRM_FLAT_MW
+    // the lanes that move are a prefix (0 .. h-1): lane i < h writes ancestor i+1 into ancestor i's
+    // place, lane h writes vk into ancestor h -- one write phase
+    if (lane <= h)
+        H[((hole + 1) >> lane) - 1] = lane < h ? ae : kv_make(vk, vi);
+#else
     if (lt) // ancestor j moves into ancestor j-1's place (ancestor 0 = the hole)
         H[((hole + 1) >> (j - 1)) - 1] = ae;
     if (lane == 0)
         H[((hole + 1) >> h) - 1] = kv_make(vk, vi);
+#endif
     return h == m;
 }
 
@@ -173,16 +184,23 @@ __device__ __forceinline__ bool par_push2(KV *Cd, int clen, KV *T, int tlen, flo
     asm volatile("" : "+v"(ca.x), "+v"(ca.y), "+v"(ta.x), "+v"(ta.y));
     const bool clt = cvalid && kv_key(ca) < -dist;
     const int hc = __popcll(bal(clt));
+    const bool tlt = tvalid && kv_key(ta) < dist;
+    const int ht = __popcll(bal(tlt));
+#if DRM_FLAT_MW
+    if (lane <= hc)
+        Cd[((chole + 1) >> lane) - 1] = lane < hc ? ca : kv_make(-dist, id);
+    if (lane <= ht)
+        T[((thole + 1) >> lane) - 1] = lane < ht ? ta : kv_make(dist, id);
+#else
     if (clt)
         Cd[((chole + 1) >> (j - 1)) - 1] = ca;
     if (lane == 0)
         Cd[((chole + 1) >> hc) - 1] = kv_make(-dist, id);
-    const bool tlt = tvalid && kv_key(ta) < dist;
-    const int ht = __popcll(bal(tlt));
     if (tlt)
         T[((thole + 1) >> (j - 1)) - 1] = ta;
     if (lane == 0)
         T[((thole + 1) >> ht) - 1] = kv_make(dist, id);
+#endif
     return ht == tm;
 }
 
@@ -223,14 +241,28 @@ template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
 {
     const int lane = lane_id_local();
     const int L = len - 1;
-    const KV ve = kv_load(H + L);
+    // every read of this round trip is issued before the first use: one LDS wait instead of one per
+    // read (left alone, the compiler waits for ve, then serialises the child reads on few VGPRs)
+    KV ve = H[L];
+    uint32_t lk[NN], rk[NN];
+#pragma unroll
+    for (int jj = 0; jj < NN; ++jj) {
+        const int p = lane + 64 * jj;
+        lk[jj] = H[2 * p + 1].x;
+        rk[jj] = H[2 * p + 2].x;
+    }
+    asm volatile("" : "+v"(ve.x), "+v"(ve.y), "+v"(lk[0]), "+v"(rk[0]));
+    if constexpr (NN > 1) {
+        asm volatile("" : "+v"(lk[1]), "+v"(rk[1]), "+v"(lk[NN - 1]), "+v"(rk[NN - 1]));
+        if constexpr (NN > 3)
+            asm volatile("" : "+v"(lk[2]), "+v"(rk[2]));
+    }
     const float vk = __uint_as_float(__builtin_amdgcn_readfirstlane(ve.x)); // uniform (ve is opaque)
     uint64_t bits[NN];
 #pragma unroll
     for (int jj = 0; jj < NN; ++jj) {
         const int p = lane + 64 * jj;
-        const KV le = H[2 * p + 1], re = H[2 * p + 2];
-        bits[jj] = bal((2 * p + 2 < L) & !(kv_key(re) < kv_key(le)));
+        bits[jj] = bal((2 * p + 2 < L) & !(__uint_as_float(rk[jj]) < __uint_as_float(lk[jj])));
     }
     const int leaf = heap_walk<NN>(bits, L);
     const int m = heap_depth(leaf);
@@ -239,19 +271,31 @@ template <int NN> __device__ __forceinline__ float par_pop(KV *H, int len)
     const KV ce = kv_load(H + (valid ? ((leaf + 1) >> (m - j)) - 1 : 0)); // P_{lane + 1}
     const int h = __popcll(bal(valid & (kv_key(ce) < vk)));
     const int t = m - h; // depth where v lands
+#if DRM_FLAT_MW
+    if (lane <= t) // P_i takes P_{i+1} for i < t, P_t takes v
+        H[((leaf + 1) >> (m - lane)) - 1] = lane < t ? ce : ve;
+#else
     if (lane < t)
         H[((leaf + 1) >> (m - lane)) - 1] = ce;
     if (lane == 0)
         H[((leaf + 1) >> h) - 1] = ve;
+#endif
     return t > 0 ? __uint_as_float(__builtin_amdgcn_readlane(ce.x, 0)) : vk;
 }
 
+#ifndef DRM_FLAT_POP3
+#define DRM_FLAT_POP3 1 // 1: three node groups for 129 .. 385-entry heaps (one child read fewer than four)
+#endif
 // heaps of up to 513 entries (the callers take the serial replay beyond)
 __device__ __forceinline__ float par_pop_any(KV *H, int len)
 {
     const int L = len - 1;
     if (L <= 128)
         return par_pop<1>(H, len);
+#if DRM_FLAT_POP3
+    if (L <= 384) // nodes 0 .. 191 (the candidate_set LDS part, 376 entries, stays below)
+        return par_pop<3>(H, len);
+#endif
     return par_pop<4>(H, len);
 }
 
