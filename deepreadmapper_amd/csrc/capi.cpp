@@ -400,7 +400,7 @@ void free_flat(drm::DeviceFlatIndex &d)
 {
     void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,    d.up,        d.labels,  d.visited,
                     d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps,
-                    d.fb_list};
+                    d.fb_list,    d.ord_state,  d.ord_keys,   d.ord_vals,  d.ord_temp};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -457,6 +457,8 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
             d.waves_per_cu = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
             d.try_sorted = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_REORDER"))
+            d.reorder = std::atoi(e); // 0 off (default), 1 on (2, 3: diagnostic splits, see launch_hnsw_flat_search)
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
             if (std::atoi(e)) {
                 DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
