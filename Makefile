@@ -16,7 +16,6 @@ HOSTFLAGS := $(COMMON) -fopenmp -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I$(ROC
 
 LIB := $(PKG)/libdrm_hip.so
 HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/hnsw_search_lds.o $(BUILD)/hnsw_flat_search.o $(BUILD)/sw_rerank.o \
-            $(BUILD)/query_order.o \
             $(BUILD)/capi.o
 HOST_OBJS := $(BUILD)/faiss_io.o $(BUILD)/formats.o $(BUILD)/builder.o $(BUILD)/embed.o $(BUILD)/hnswlib_io.o \
              $(BUILD)/builder_flat.o

@@ -286,7 +286,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--build-threads", type=int, default=0)
-    ap.add_argument("--index", choices=["pq", "flat"], default="flat",
+    ap.add_argument("--index", choices=["pq", "flat"], default="pq",
                     help="flat (default): hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib "
                          "defaults), configs[1]'s L2 HNSW search; pq: faiss IndexHNSWPQ, the live pipeline's index")
     ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
@@ -439,7 +439,9 @@ def main():
             "value": round(value, 1), "unit": "reads/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("fp32 (L2 distances)" if flat else "fp32 (PQ-ADC distances)") + " + int32 (SW DP)",
+            "dtype": ("fp32 (L2 distances)" if flat else "fp32 (PQ-ADC distances)") + (
+                " + int32 (SW DP, bit-profile u16 kernel)" if os.environ.get("DRM_SW_BITPROFILE") == "1" else
+                " + fp16 fixed-point SW DP (2^-10 units, exact for scores < 1024)"),
             "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
             "config": {"workload": workload, "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},

@@ -400,7 +400,7 @@ void free_flat(drm::DeviceFlatIndex &d)
 {
     void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,    d.up,        d.labels,  d.visited,
                     d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps,
-                    d.fb_list,    d.ord_state,  d.ord_keys,   d.ord_vals,  d.ord_temp};
+                    d.fb_list};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -457,8 +457,6 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
             d.waves_per_cu = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
             d.try_sorted = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_REORDER"))
-            d.reorder = std::atoi(e); // 0 off (default), 1 on (2, 3: diagnostic splits, see launch_hnsw_flat_search)
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
             if (std::atoi(e)) {
                 DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
@@ -518,6 +516,8 @@ int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, i
             throw Error(DRM_ERR_ARG, "null argument");
         if (n <= 0)
             throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswlib_dir/search.cpp:20-23
+        if (n >= (int64_t)1 << 31)
+            throw Error(DRM_ERR_ARG, "more than 2^31-1 queries in one call");
         DRM_HIP_CHECK(hipSetDevice(index->dev.device));
         drm::launch_hnsw_flat_search(index->dev, d_x, n, k, ef, d_D, d_labels, d_ndis, d_nhops, d_nhops_upper,
                                      (hipStream_t)stream);
@@ -570,6 +570,8 @@ int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d,
             throw Error(DRM_ERR_ARG, "null argument");
         if (n <= 0)
             throw Error(DRM_ERR_ARG, "Query data is empty"); // src/hnswlib_dir/search.cpp:20-23
+        if (n >= (int64_t)1 << 31)
+            throw Error(DRM_ERR_ARG, "more than 2^31-1 queries in one call");
         if (d != index->dev.d)
             throw Error(DRM_ERR_ARG, "query dimension " + std::to_string(d) + " != index dimension " +
                                          std::to_string(index->dev.d));

@@ -123,15 +123,6 @@ struct DeviceFlatIndex {
     int32_t *fb_list = nullptr;     // queries the tie-free pass handed to the exact pass
     int64_t fb_cap = 0;
     uint64_t *stamps = nullptr;     // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
-    // query order (DRM_SEARCH_REORDER=1, default off: measured slower): a descent-only pass, then the
-    // level-0 pass takes the queries sorted by their level-0 entry node
-    int32_t reorder = 0;
-    int64_t ord_cap = 0;
-    int4 *ord_state = nullptr;      // [cap] (entry node, its distance bits, ndis, upper hops) per query
-    uint32_t *ord_keys = nullptr;   // [2 cap] entry node per query, then sorted
-    int32_t *ord_vals = nullptr;    // [2 cap] query ids, then in key order (the level-0 queue)
-    void *ord_temp = nullptr;       // radix-sort scratch
-    size_t ord_temp_bytes = 0;
     int64_t device_bytes = 0;
     HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
 };
@@ -175,15 +166,7 @@ struct FlatArgs {
     int32_t *fb_list;     // tie-free pass: queries that met a distance tie
     uint32_t *fb_count;
     uint32_t *overflow;   // candidate_set overflow count (counter[1])
-    int4 *ord_state;      // query order (kernel MODE 1 writes, MODE 2 reads)
-    uint32_t *ord_keys;
-    int32_t *ord_vals;
 };
-
-// radix sort of (u32 key, i32 value) pairs on the low `bits` key bits (hipCUB), query_order.hip
-size_t sort_pairs_temp_bytes(int64_t n, int bits);
-void sort_pairs(void *temp, size_t temp_bytes, const uint32_t *kin, uint32_t *kout, const int32_t *vin, int32_t *vout,
-                int64_t n, int bits, hipStream_t stream);
 
 void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D,
                              uint64_t *d_L, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper,

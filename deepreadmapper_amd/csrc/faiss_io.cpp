@@ -178,6 +178,16 @@ void validate_hnswpq(const HnswPqHost &ix)
     for (int32_t v : ix.neighbors)
         if (v < -1 || v >= n)
             bad("neighbor id " + std::to_string(v) + " out of range");
+    // a level-l link must point at a node that exists on level l: the search reads the target's
+    // level-l list, which is only laid out for nodes with levels[target] > l
+    for (int64_t i = 0; i < n; ++i)
+        for (int l = 1; l < ix.levels[i]; ++l)
+            for (int32_t j = ix.cum_nneighbor_per_level[l]; j < ix.cum_nneighbor_per_level[l + 1]; ++j) {
+                const int32_t v = ix.neighbors[ix.offsets[i] + (uint64_t)j];
+                if (v >= 0 && ix.levels[v] <= l)
+                    bad("node " + std::to_string(i) + " links to node " + std::to_string(v) + " on level " +
+                        std::to_string(l) + ", which that node does not reach");
+            }
     if (n > 0) {
         if (ix.entry_point < 0 || ix.entry_point >= n)
             bad("entry_point out of range");

@@ -657,8 +657,7 @@ __device__ __forceinline__ void bitonic128(float (&k)[2], uint64_t (&l)[2])
 
 // NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
 // NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
-// MODE 0: the whole search; 1: upper-level descent only (state + order key to ord_*); 2: level 0 from
-// ord_state, queue order from qlist.
+// MODE 0: the whole search (the only mode).
 template <int NV, int NR, bool STAMPS, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAVES))) void hnsw_flat_search_kernel(FlatArgs a)
 {
@@ -720,18 +719,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
         }
         __syncthreads();
         int ndis = 0, nhops = 0;
-        // --- searchKnn: greedy descent on levels maxlevel .. 1 (mode 2: done by the mode-1 pass,
-        // whose end state is picked up here)
+        // --- searchKnn: greedy descent on levels maxlevel .. 1
         uint32_t cur = a.ep;
         float curdist = 0.0f;
         int nhops_up = 0;
-        if constexpr (MODE == 2) {
-            const int4 stt = a.ord_state[qi];
-            cur = (uint32_t)__builtin_amdgcn_readfirstlane(stt.x);
-            curdist = __int_as_float(__builtin_amdgcn_readfirstlane(stt.y));
-            ndis = __builtin_amdgcn_readfirstlane(stt.z);
-            nhops_up = nhops = __builtin_amdgcn_readfirstlane(stt.w);
-        } else {
+        {
             if (lane == 0)
                 fid[0] = cur;
             __syncthreads();
@@ -739,7 +731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
             curdist = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fd[0])));
             ndis++;
         }
-        for (int level = MODE == 2 ? 0 : a.maxlevel; level > 0; --level) {
+        for (int level = a.maxlevel; level > 0; --level) {
             for (;;) {
                 const uint32_t *blk = a.up + a.up_off[cur] + (int64_t)(level - 1) * (1 + a.maxM);
                 const int size = (int)(blk[0] & 0xFFFFu);
@@ -764,13 +756,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
                     break;
             }
         }
-        if constexpr (MODE == 1) { // descent pass: end state + the level-0 entry as the query-order key
-            // (every lane stores the same words: no lane-divergent region -- with one plus a `continue`
-            // the loop's exit mask came out per lane and the wave hung)
-            a.ord_state[qi] = make_int4((int)cur, __float_as_int(curdist), ndis, nhops_up);
-            a.ord_keys[qi] = cur;
-            a.ord_vals[qi] = qi;
-        } else {
+        {
         // --- searchBaseLayerST<bare_bone_search = true>(cur, q, max(ef, k))
         int clear_n = 1;
         if (lane == 0) {
@@ -1102,7 +1088,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
         }
         __syncthreads();
         FLAT_STAMP(5); // result ordering + reset
-        } // MODE != 1
+        }
     }
     if (STAMPS && lane == 0 && a.stamps)
         for (int i = 0; i < 8; ++i)
@@ -1233,49 +1219,6 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         a.counter = ix.counter + 3;
         a.stamps = nullptr;
     }
-    // query order (DRM_SEARCH_REORDER=1; off by default): the upper-level descent of every query first
-    // (mode 1), then the level-0 searches (mode 2) in the order of their entry node ids, so the ~8k
-    // queries resident at a time search neighbouring graph regions and might share rows and vectors in
-    // L2 / the Infinity Cache. Results do not depend on it. Measured slower on C3 (12.36-12.40 ms vs
-    // 11.76-11.82 ms in one-box A/B): the entry nodes of random queries are spread over the whole graph
-    // and the extra pass + sort costs more than the locality returns.
-    const bool reorder = !sorted_pass && ix.reorder && n >= 1024 && ix.ntotal > 0 && ix.ntotal <= 0xFFFFFFFFll;
-    if (reorder) {
-        const int bits = std::max(1, 64 - __builtin_clzll((unsigned long long)(ix.ntotal - 1) | 1ull));
-        const size_t tb = sort_pairs_temp_bytes(n, bits);
-        if (n > ix.ord_cap || tb > ix.ord_temp_bytes) {
-            for (void *p : {(void *)ix.ord_state, (void *)ix.ord_keys, (void *)ix.ord_vals, ix.ord_temp})
-                if (p)
-                    DRM_HIP_CHECK(hipFree(p));
-            ix.ord_cap = std::max(n, ix.ord_cap);
-            DRM_HIP_CHECK(hipMalloc(&ix.ord_state, sizeof(int4) * (size_t)ix.ord_cap));
-            DRM_HIP_CHECK(hipMalloc(&ix.ord_keys, 2 * sizeof(uint32_t) * (size_t)ix.ord_cap));
-            DRM_HIP_CHECK(hipMalloc(&ix.ord_vals, 2 * sizeof(int32_t) * (size_t)ix.ord_cap));
-            ix.ord_temp_bytes = std::max(tb, sort_pairs_temp_bytes(ix.ord_cap, 32));
-            DRM_HIP_CHECK(hipMalloc(&ix.ord_temp, ix.ord_temp_bytes));
-        }
-        a.ord_state = ix.ord_state;
-        a.ord_keys = ix.ord_keys;
-        a.ord_vals = ix.ord_vals;
-        uint64_t *stamps = a.stamps;
-        a.stamps = nullptr;
-        if (ix.d == 128)
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, false, 1>), dim3(slots), dim3(64), lds, stream, a);
-        else
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, false, 1>), dim3(slots), dim3(64), lds, stream, a);
-        DRM_HIP_CHECK(hipGetLastError());
-        if (ix.reorder != 3)
-            sort_pairs(ix.ord_temp, ix.ord_temp_bytes, ix.ord_keys, ix.ord_keys + ix.ord_cap, ix.ord_vals,
-                       ix.ord_vals + ix.ord_cap, n, bits, stream);
-        else
-            DRM_HIP_CHECK(hipMemcpyAsync(ix.ord_vals + ix.ord_cap, ix.ord_vals, sizeof(int32_t) * (size_t)n,
-                                         hipMemcpyDeviceToDevice, stream));
-        DRM_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(ix.counter + 5), (int)n, 1, stream));
-        a.qlist = ix.ord_vals + ix.ord_cap;
-        a.qcount = ix.counter + 5;
-        a.counter = ix.counter + 4;
-        a.stamps = stamps;
-    }
 #define DRM_FLAT_MAIN(M_)                                                                                      \
     if (ix.d == 128) {                                                                                          \
         if (a.stamps)                                                                                           \
@@ -1288,11 +1231,7 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         else                                                                                                    \
             hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
     }
-    if (reorder && ix.reorder != 2) {
-        DRM_FLAT_MAIN(2)
-    } else {
-        DRM_FLAT_MAIN(0)
-    }
+    DRM_FLAT_MAIN(0)
 #undef DRM_FLAT_MAIN
     DRM_HIP_CHECK(hipGetLastError());
 }

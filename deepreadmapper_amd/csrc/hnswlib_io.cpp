@@ -128,13 +128,22 @@ HnswFlatHost read_hnswlib(const std::string &path)
             if (row[1 + j] >= n)
                 throw bad("level-0 link out of range at element " + std::to_string(i));
     }
-    for (size_t b = 0; b < ix.up.size(); b += blk) {
-        if ((ix.up[b] & 0xFFFFu) > ix.maxM)
-            throw bad("upper link count > maxM");
-        for (uint32_t j = 0; j < (ix.up[b] & 0xFFFFu); ++j)
-            if (ix.up[b + 1 + j] >= n)
-                throw bad("upper link out of range");
-    }
+    // block l-1 of node i lists its level-l links; every target must itself reach level l (the
+    // search reads the target's level-l block, which only exists for levels[target] >= l)
+    for (uint64_t i = 0; i < n; ++i)
+        for (int32_t l = 1; l <= ix.levels[i]; ++l) {
+            const size_t b = (size_t)ix.up_off[i] + (size_t)(l - 1) * blk;
+            if ((ix.up[b] & 0xFFFFu) > ix.maxM)
+                throw bad("upper link count > maxM");
+            for (uint32_t j = 0; j < (ix.up[b] & 0xFFFFu); ++j) {
+                const uint32_t v = ix.up[b + 1 + j];
+                if (v >= n)
+                    throw bad("upper link out of range");
+                if (ix.levels[v] < l)
+                    throw bad("element " + std::to_string(i) + " links to element " + std::to_string(v) +
+                              " on level " + std::to_string(l) + ", which that element does not reach");
+            }
+        }
     if (n > 0 && ix.levels[ix.ep] != ix.maxlevel)
         throw bad("entry point is not on the top level");
     return ix;

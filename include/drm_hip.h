@@ -25,6 +25,11 @@ extern "C" {
 #define DRM_ERR_K (-6)         /* "Final k too large..."           src/utils/post_processor.cpp:486-489 */
 #define DRM_ERR_UNSUPPORTED (-7)
 
+/* Threading: every handle (drm_index, drm_flat_index, drm_refs) owns mutable device scratch (visited
+ * bitmaps, clear lists, queue counters, rerank workspace). A handle is single-stream: its calls must be
+ * serialised in stream order (one in-flight call per handle). Concurrent work on one device uses one
+ * handle per stream; multi-device fan-out (drm_multi_*) keeps one handle per device. The diagnostic
+ * counters (drm_*_overflows / _fallbacks) describe the handle's most recent search. */
 typedef struct drm_index drm_index; /* device-resident IndexHNSWPQ */
 typedef struct drm_refs drm_refs;   /* device-resident static window table (ref_seqs) */
 

@@ -104,3 +104,69 @@ def test_hnswpq_index_cli(tmp_path):
     assert fx.ntotal == 1702
     r = subprocess.run([exe, fna], capture_output=True, text=True)
     assert r.returncode == 1 and "Usage" in r.stderr
+
+
+def test_index_load_rejects_upper_link_to_lower_node(tmp_path, c1):
+    """A level-l link must target a node that reaches level l (faiss IHNp): the kernel would read
+    the target's level-l list, which does not exist. Rejected as DRM_ERR_FORMAT before any GPU use."""
+    from deepreadmapper_amd import read_index, DrmError
+    from deepreadmapper_amd._native import DRM_ERR_FORMAT
+    fx = c1["fx"]
+    lv, cum, offs = fx.levels, fx.cum_nneighbor_per_level, fx.offsets
+    pos = 4 + 33 + (8 + 8 * len(fx.assign_probas)) + (8 + 4 * len(cum)) + (8 + 4 * len(lv)) + (8 + 8 * len(offs)) + 8
+    src = int(np.flatnonzero(lv >= 2)[0])
+    low = int(np.flatnonzero(lv == 1)[0])
+    slot = int(offs[src]) + int(cum[1])  # first level-1 link of src
+    data = bytearray(open(c1["index"], "rb").read())
+    data[pos + 4 * slot: pos + 4 * slot + 4] = np.int32(low).tobytes()
+    bad = tmp_path / "uplink.index"
+    bad.write_bytes(bytes(data))
+    with pytest.raises(DrmError) as e:
+        read_index(str(bad))
+    assert e.value.code == DRM_ERR_FORMAT and "does not reach" in str(e.value)
+
+
+def test_flat_index_load_rejects_upper_link_to_lower_node(tmp_path):
+    """Same check on the hnswlib reader (an upper link to a level-0 element)."""
+    from deepreadmapper_amd import synth, DrmError
+    from deepreadmapper_amd.flat import HnswFlatIndex
+    from deepreadmapper_amd._native import DRM_ERR_FORMAT
+    from oracle import hnswlib_file
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((3000, 16)).astype(np.float32)
+    path = str(tmp_path / "f.hnsw")
+    synth.build_flat_index(x, path, M=8, efc=32, nthreads=1)
+    fx = hnswlib_file.read(path)
+    n, maxM0, maxM, d = fx["n"], fx["maxM0"], fx["maxM"], fx["d"]
+    sz_el = 4 * (1 + maxM0) + 4 * d + 8
+    pos = 96 + n * sz_el
+    low = int(np.flatnonzero(fx["levels"] == 0)[0])
+    data = bytearray(open(path, "rb").read())
+    for i in range(n):
+        size = int(np.frombuffer(data[pos:pos + 4], np.uint32)[0])
+        pos += 4
+        if size and int(np.frombuffer(data[pos:pos + 4], np.uint32)[0]) & 0xFFFF:
+            data[pos + 4:pos + 8] = np.uint32(low).tobytes()  # first level-1 link
+            break
+        pos += size
+    bad = tmp_path / "bad.hnsw"
+    bad.write_bytes(bytes(data))
+    with pytest.raises(DrmError) as e:
+        HnswFlatIndex(str(bad))
+    assert e.value.code == DRM_ERR_FORMAT and "does not reach" in str(e.value)
+
+
+def test_pipeline_rejects_ragged_reference(tmp_path):
+    """a .txt reference with a line shorter than ref_len is refused with a format
+    error before the GPU is touched (the fixed-width window table would over-read it)."""
+    exe = os.path.join(ROOT, "bin", "pipeline")
+    prefix = tmp_path / "idx"
+    prefix.mkdir()
+    (prefix / "config.txt").write_text("ref_len: 150\nstride: 1\n")
+    (prefix / "idx.index").write_bytes(b"")
+    ref = tmp_path / "ref.txt"
+    ref.write_text("A" * 150 + "\n" + "C" * 149 + "\n")
+    q = tmp_path / "q.txt"
+    q.write_text("A" * 150 + "\n")
+    r = subprocess.run([exe, str(prefix), str(q), str(ref)], capture_output=True, text=True)
+    assert r.returncode == 1 and "reference sequence 1 has 149 bytes" in r.stderr

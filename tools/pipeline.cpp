@@ -109,6 +109,15 @@ int main(int argc, char *argv[])
             std::vector<std::string> dummy;
             drm::read_file(ref_file, refs, dummy, ref_len, 1, true);
             std::cout << "[MAIN] Loaded " << refs.size() << " reference sequences from " << ref_file << std::endl;
+            // the device window table is fixed-width: a .txt / .fastq reference whose lines are not
+            // all ref_len bytes would be over-read or silently truncated (the reference scores the
+            // whole string), so it is refused before anything touches the GPU
+            for (size_t r = 0; r < refs.size(); ++r)
+                if (refs[r].size() != ref_len)
+                    throw drm::Error(DRM_ERR_FORMAT, "reference sequence " + std::to_string(r) + " has " +
+                                                         std::to_string(refs[r].size()) +
+                                                         " bytes; the window table needs ref_len = " +
+                                                         std::to_string(ref_len) + " for every window");
         }
         std::cout << "[MAIN] Total Data loading time: " << ms_since(t0) << " ms" << std::endl << std::endl;
 
