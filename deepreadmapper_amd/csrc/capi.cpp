@@ -78,7 +78,7 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 void free_index(drm::DeviceIndex &d)
 {
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr,
-                    d.visited,   d.clear_list, d.counter, d.stamps,   d.fb_list};
+                    d.visited,   d.clear_list, d.counter, d.stamps,   d.fb_list, d.log};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -232,6 +232,10 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.force_exact = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("DRM_SEARCH_LOG_CAP"))
+            d.log_cap_req = std::max(1, std::atoi(e));
+        if (const char *e = std::getenv("DRM_SEARCH_FAST"))
+            d.use_fast = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
             d.try_sorted = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))

@@ -48,6 +48,10 @@ struct DeviceIndex {
     uint32_t *counter = nullptr;   // [0] work queue head, [1] fallback count, [2] fallback queue head
     int32_t *fb_list = nullptr;    // queries the sorted-array pass handed to the exact kernel
     int64_t fb_cap = 0;
+    int32_t use_fast = 1;          // lean kernel (hnsw_pq_fast.hip) where it applies; DRM_SEARCH_FAST=0 off
+    uint64_t *log = nullptr;       // [n_slots][log_cap] accepted pushes (lean kernel, k == ef)
+    int32_t log_cap = 0, log_slots = 0;
+    int32_t log_cap_req = 2048;    // entries per slot (DRM_SEARCH_LOG_CAP; >= ef + 64, compaction beyond)
     int64_t device_bytes = 0;
     HnswPqHost meta; // header fields kept for drm_index_get_info (vectors released)
 };
@@ -83,7 +87,13 @@ struct SearchArgs {
     const uint32_t *qcount;
     int32_t *fb_list;      // sorted-array kernel: queries handed to the exact kernel
     uint32_t *fb_count;
+    uint64_t *log;         // lean kernel: per-slot log of accepted MinimaxHeap pushes
+    int32_t log_cap;
 };
+
+// lean kernel (hnsw_pq_fast.hip): PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64
+bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc);
+void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream);
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);

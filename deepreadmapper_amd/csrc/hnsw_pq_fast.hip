@@ -1,0 +1,532 @@
+// deepreadmapper_amd/csrc/hnsw_pq_fast.hip -- lean HNSW-PQ search kernel for the common shape
+// (PQ 8 x 8 bits, level-0 degree <= 64, ef <= 128), bit-identical to the exact kernel in
+// hnsw_search.hip and to the oracle (faiss IndexHNSW::search -> HNSW::search ->
+// search_from_candidates with MinimaxHeap + HeapBlockResultHandler [upstream faiss >= 1.8],
+// restated in oracle/drm_oracle.c). Caller: faiss_search (src/hnswpq/search.cpp:39-40).
+//
+// What makes it lean ("hnsw_pq_fast_kernel"):
+//   * every MinimaxHeap slot is one u64 = (ord32(distance) << 32) | (id ^ 2^31): faiss's cmp2 on
+//     (distance, id) -- popped slots carry id -1 -- becomes a single unsigned 64-bit compare;
+//   * the heap sits in the sibling-pair layout (lane p holds the children of node p, slots 2p+1 and
+//     2p+2; the root is lane 63's second half). heap_pop finds the sift-down path by pointer doubling
+//     (3 ds_bpermute) and heap_push the sift-up chain by one parallel ancestor fetch: no scalar walks;
+//   * pop_min is one 32-bit DPP min plus a ballot for the highest tied slot;
+//   * result set at k == ef: the HeapBlockResultHandler (k = ef) holds, at every step, the same
+//     multiset of distances as the MinimaxHeap (both start empty, both accept everything until they
+//     hold ef entries, then both take d < (their common) maximum and drop one maximum). Its final
+//     content is therefore the k smallest (distance, id) pairs among the pushes the MinimaxHeap
+//     accepted, with the MinimaxHeap's final root distance T as the k-th distance. The kernel logs
+//     every accepted push (one masked store per hop) instead of maintaining the result heap, and
+//     selects + sorts the k results once per query. k < ef keeps a register result set (k <= 64).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "drm_device.h"
+#include "pq_common.h"
+
+#pragma clang fp contract(off)
+
+namespace drm {
+namespace {
+
+constexpr uint32_t kPopLo = 0x7FFFFFFFu;            // low word of a popped slot (id -1 ^ 2^31)
+constexpr uint64_t kUnused = 0xFFFFFFFF7FFFFFFFull; // key above every distance, popped
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint64_t pack(uint32_t key, int32_t id)
+{
+    return ((uint64_t)key << 32) | (uint32_t)((uint32_t)id ^ 0x80000000u);
+}
+__device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+__device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+__device__ __forceinline__ int32_t unpack_id(uint64_t v) { return (int32_t)(lo32(v) ^ 0x80000000u); }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hi32(v), l);
+    const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)lo32(v), l);
+    return ((uint64_t)h << 32) | o;
+}
+__device__ __forceinline__ uint32_t bperm32(uint32_t v, int src)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src)
+{
+    return ((uint64_t)bperm32(hi32(v), src) << 32) | bperm32(lo32(v), src);
+}
+__device__ __forceinline__ int bitlen(uint32_t x) { return 32 - __builtin_clz(x); } // x >= 1
+__device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // lane i <- lane i-1
+{
+    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)hi32(old), (int)hi32(v), 0x138, 0xF, 0xF, false);
+    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)lo32(old), (int)lo32(v), 0x138, 0xF, 0xF, false);
+    return ((uint64_t)h << 32) | o;
+}
+
+// MinimaxHeap arrays (ef <= 128) in the sibling-pair layout.
+struct Heap {
+    uint64_t L, R;
+
+    // value of slot s (wave-uniform s)
+    __device__ __forceinline__ uint64_t get(int s) const
+    {
+        if (s == 0)
+            return readlane64(R, 63);
+        const int o = (s - 1) >> 1;
+        return (s & 1) ? readlane64(L, o) : readlane64(R, o);
+    }
+
+    // faiss heap_pop<CMax<float, int>>(k): slot k-1 sifted down from the root (1-based k >= 1).
+    __device__ __forceinline__ void pop(int k, int lane)
+    {
+        const uint64_t val = get(k - 1);
+        const bool has_l = 2 * lane + 1 <= k - 1;
+        const bool has_r = 2 * lane + 2 <= k - 1 && lane != 63;
+        const bool takeL = !has_r || L > R;                 // (i2 == k + 1) || cmp2(heap[i1], heap[i2])
+        const int ch = takeL ? 2 * lane + 1 : 2 * lane + 2; // chosen child slot
+        const uint64_t chv = takeL ? L : R;
+        const bool moves = has_l && !(val > chv);           // the child moves up unless cmp2(val, child)
+        // next hole position, pointer-doubled: n8(0) is the final hole (depth <= 7)
+        const int n1 = moves ? ch : lane;
+        int n = n1;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int t = (int)bperm32((uint32_t)n, n & 63);
+            n = n < 64 ? t : n;
+        }
+        const int hole = __builtin_amdgcn_readlane(n, 0);
+        // lanes strictly above the hole on its root path moved their chosen child up
+        const uint32_t hx = (uint32_t)hole + 1u;
+        const int sh = bitlen(hx) - bitlen((uint32_t)lane + 1u);
+        const bool writer = sh > 0 && (hx >> sh) == (uint32_t)lane + 1u;
+        const uint64_t up = bperm64(chv, ch & 63);
+        const uint64_t nv = (ch == hole) ? val : up;
+        if (writer && takeL)
+            L = nv;
+        if (writer && !takeL)
+            R = nv;
+        const uint64_t rootv = hole != 0 ? readlane64(chv, 0) : val;
+        if (lane == 63)
+            R = rootv;
+    }
+
+    // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
+    __device__ __forceinline__ void push(int k, uint64_t val, int lane)
+    {
+        // lane j in [1, 7] looks at the ancestor a_j = k >> j (1-based)
+        const int aj = (lane >= 1 && lane < 8) ? (k >> lane) : 0;
+        const int t = aj - 1; // its slot
+        const int owner = t <= 0 ? 63 : (t - 1) >> 1;
+        const bool sideR = t <= 0 || !(t & 1);
+        const uint64_t fl = bperm64(L, owner), fr = bperm64(R, owner);
+        const uint64_t av = sideR ? fr : fl;
+        const bool moves = aj >= 1 && val > av; // cmp2(val, father): the father moves down
+        const int h = __builtin_popcountll(ballot(moves)); // ancestors 1..h move (heap order: a prefix)
+        // chain index m (a_m = k >> m, m = 0..h) gets a_{m+1}'s value, or val at m == h
+        const int bk = bitlen((uint32_t)k);
+        const uint32_t xl = 2u * (uint32_t)lane + 2u, xr = xl + 1u; // 1-based indices of L, R
+        const int ml = bk - bitlen(xl), mr = bk - bitlen(xr);
+        const bool onL = ml >= 0 && ml <= h && (uint32_t)(k >> ml) == xl;
+        const bool onR = lane != 63 && mr >= 0 && mr <= h && (uint32_t)(k >> mr) == xr;
+        const int m = onL ? ml : mr;
+        const uint64_t pulled = bperm64(av, (m + 1) & 63);
+        const uint64_t nv = (m == h) ? val : pulled;
+        if (onL)
+            L = nv;
+        if (onR)
+            R = nv;
+        // the root (lane 63 R, 1-based 1 = a_{bk-1}) changes only if val climbs all the way up
+        if (h == bk - 1 && lane == 63)
+            R = val;
+    }
+};
+
+// bitonic sort of 128 u64 (lane l holds elements l and l + 64), ascending
+__device__ __forceinline__ void sort128(uint64_t &x0, uint64_t &x1, int lane)
+{
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride == 64) {
+                // partner of element lane is element lane + 64; ascending block (size == 128)
+                const uint64_t lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
+                x0 = lo;
+                x1 = hi;
+            } else {
+                const int pl = lane ^ stride;
+                const uint64_t p0 = bperm64(x0, pl), p1 = bperm64(x1, pl);
+                const bool lower = (lane & stride) == 0;
+                const bool asc0 = (lane & size) == 0;         // element index lane
+                const bool asc1 = ((lane + 64) & size) == 0;  // element index lane + 64
+                const bool keepmin0 = lower == asc0, keepmin1 = lower == asc1;
+                x0 = keepmin0 ? (x0 < p0 ? x0 : p0) : (x0 < p0 ? p0 : x0);
+                x1 = keepmin1 ? (x1 < p1 ? x1 : p1) : (x1 < p1 ? p1 : x1);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t log_load(const uint64_t *lg, int i)
+{
+    return __hip_atomic_load(lg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The k (= ef) results among the log of accepted pushes: every entry with key < T, then the
+// smallest (packed) ids among key == T up to k in all. T = ~0 when the heap never filled (all).
+// Returns the largest packed low word admitted at key == T.
+__device__ uint32_t log_id_threshold(const uint64_t *lg, int logn, uint32_t T, int k, int lane)
+{
+    __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed before it reads them back
+    int nlt = 0, neq = 0;
+    for (int b = 0; b < logn; b += 64) {
+        const int i = b + lane;
+        const uint64_t e = i < logn ? log_load(lg, i) : ~0ull;
+        nlt += __builtin_popcountll(ballot(i < logn && hi32(e) < T));
+        neq += __builtin_popcountll(ballot(i < logn && hi32(e) == T));
+    }
+    const int need = k - nlt;
+    if (T == 0xFFFFFFFFu || neq <= need)
+        return 0xFFFFFFFFu;
+    // rare: more entries at distance T than places -- binary search the need-th smallest low word
+    uint32_t lo = 0u, hi = 0xFFFFFFFFu;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+        for (int b = 0; b < logn; b += 64) {
+            const int i = b + lane;
+            const uint64_t e = i < logn ? log_load(lg, i) : ~0ull;
+            c += __builtin_popcountll(ballot(i < logn && hi32(e) == T && lo32(e) <= mid));
+        }
+        if (c >= need)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+// Copies the selected log entries, in log order, to dst[0 .. count) and returns count (<= k).
+// dst may be the log itself (in-place compaction: a block is read before any write can reach it).
+template <typename Ptr>
+__device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t T, uint32_t idthr, Ptr dst, int lane)
+{
+    int cnt = 0;
+    for (int b = 0; b < logn; b += 64) {
+        const int i = b + lane;
+        const uint64_t e = i < logn ? log_load(lg, i) : ~0ull;
+        const bool sel = i < logn && (hi32(e) < T || (hi32(e) == T && lo32(e) <= idthr));
+        const uint64_t sm = ballot(sel);
+        if (sel)
+            dst(cnt + __builtin_popcountll(sm & lanes_below(lane)), e);
+        cnt += __builtin_popcountll(sm);
+    }
+    return cnt;
+}
+
+#define DRM_FSTAMP(idx)                                                                                     \
+    do {                                                                                                    \
+        if (STAMPS) {                                                                                       \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                                               \
+            __builtin_amdgcn_sched_barrier(0);                                                              \
+            st_acc[idx] += _t - st_last;                                                                    \
+            st_last = _t;                                                                                   \
+        }                                                                                                   \
+    } while (0)
+
+// LOGRES: k == ef (result set from the log); else k <= 64 (register result set).
+template <bool LOGRES, bool STAMPS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    const int lane = lane_id();
+    float *lut = reinterpret_cast<float *>(smem);
+    uint64_t *stage = reinterpret_cast<uint64_t *>(smem); // reuses the LUT once the walk is over
+    uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
+    int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
+    uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
+    const int ef = a.ef, k = a.k, deg0 = a.deg0;
+    const uint32_t kInfKey = ord32(INFINITY);
+
+    for (;;) {
+        int q = 0;
+        if (lane == 0)
+            q = (int)atomicAdd(a.counter, 1u);
+        q = __builtin_amdgcn_readfirstlane(q);
+        if ((int64_t)q >= a.n)
+            break;
+        if (a.entry_point < 0 || a.ntotal == 0) {
+            for (int j = lane; j < k; j += 64) {
+                a.D[(int64_t)q * k + j] = INFINITY;
+                a.I[(int64_t)q * k + j] = -1;
+            }
+            if (lane == 0) {
+                a.ndis[q] = 0;
+                a.nhops[q] = 0;
+                if (a.nhops_upper)
+                    a.nhops_upper[q] = 0;
+            }
+            continue;
+        }
+        DRM_FSTAMP(7);
+        if (a.x_aligned16)
+            build_lut_m8(a, q, lut, lane);
+        else
+            build_lut(a, q, lut, lane);
+        DRM_FSTAMP(0);
+        int32_t nearest;
+        uint32_t dn;
+        int ndis, nhops;
+        greedy_upper<true>(a, lut, lane, nearest, dn, ndis, nhops);
+        const int nhops_upper = nhops;
+        DRM_FSTAMP(1);
+
+        // MinimaxHeap candidates(ef); candidates.push(nearest, d_nearest)
+        Heap hp;
+        hp.L = kUnused;
+        hp.R = lane == 63 ? pack(dn, nearest) : kUnused;
+        int kc = 1, nvalid = 1;
+        uint64_t root = pack(dn, nearest); // slot 0
+        // result set: the log (LOGRES) or a sorted register set of k <= 64 entries
+        int logn = 0;
+        uint64_t rv = ~0ull; // !LOGRES: lane j < k holds the j-th smallest (key, id) so far
+        uint32_t thr = kInfKey;
+        auto add_result = [&](uint64_t v) { // SingleResultHandler::add_result, k <= 64
+            const int pos = __builtin_popcountll(ballot(lane < k && rv < v));
+            const uint64_t sh = dpp_shr1_u64(~0ull, rv);
+            rv = lane > pos ? sh : (lane == pos ? v : rv);
+            thr = (uint32_t)__builtin_amdgcn_readlane((int)hi32(rv), k - 1);
+        };
+        if (LOGRES) {
+            if (lane == 0)
+                lg[0] = root;
+            logn = 1;
+        } else {
+            if (dn < thr)
+                add_result(root);
+        }
+        if (lane == 0) {
+            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
+            if (a.clear_cap > 0)
+                clr[0] = nearest;
+        }
+        int clear_n = 1;
+        int nstep = 0, ndis0 = 0;
+        int32_t pred = -1, v1_pref = -1;
+        while (nvalid > 0) {
+            // pop_min: smallest key among valid slots, ties -> the highest slot
+            const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
+            const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
+            // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest
+            const bool pickR = lane != 63 ? cR <= cL : cR < cL;
+            const uint32_t pk = pickR ? cR : cL;
+            const uint32_t d0 = wave_min_u32(pk);
+            const uint64_t tiedm = ballot(pk == d0 && !(lane == 63 && pickR));
+            const uint64_t rightm = ballot(pickR);
+            int wl = 63;
+            bool wR = true;
+            if (tiedm) {
+                wl = 63 - __builtin_clzll(tiedm);
+                wR = (rightm >> wl) & 1ull;
+            }
+            const int32_t v0 = (int32_t)((uint32_t)__builtin_amdgcn_readlane((int)lo32(wR ? hp.R : hp.L), wl) ^
+                                         0x80000000u);
+            if (lane == wl) {
+                if (wR)
+                    hp.R = (hp.R & ~0xFFFFFFFFull) | kPopLo;
+                else
+                    hp.L = (hp.L & ~0xFFFFFFFFull) | kPopLo;
+            }
+            if (wl == 63 && wR)
+                root = (root & ~0xFFFFFFFFull) | kPopLo;
+            nvalid--;
+            // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
+            const int below = __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
+            if (below >= a.efSearch)
+                break;
+            DRM_FSTAMP(2);
+
+            // expand v0's level-0 row (one coalesced load, lane j = link j)
+            int32_t v1 = v1_pref;
+            if (v0 != pred)
+                v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
+            const uint64_t negm = ballot(lane < deg0 && v1 < 0);
+            const int jmax = negm ? __builtin_ctzll(negm) : deg0;
+            const bool act = lane < jmax;
+            uint2 c8 = make_uint2(0u, 0u);
+            uint32_t old = 0xFFFFFFFFu;
+            const uint32_t bit = 1u << (v1 & 31);
+            if (act) {
+                c8 = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1 * 8); // overlaps the visited test
+                old = vis_test_set(&vis[v1 >> 5], bit);
+            }
+            bool fresh = act && (old & bit) == 0u;
+            if (a.check_dups) { // a repeated id in one row: only its first occurrence is fresh
+                for (int j = 0; j < jmax; ++j) {
+                    const int32_t vj = __shfl(v1, j, 64);
+                    if (j < lane && vj == v1)
+                        fresh = false;
+                }
+            }
+            DRM_FSTAMP(3);
+            const uint64_t fm = ballot(fresh);
+            const int nf = __builtin_popcountll(fm);
+            ndis0 += nf;
+            // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
+            // on the fresh ones)
+            float r = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                r = __fadd_rn(r, lut[m * 256 + ((c8.x >> (8 * m)) & 255u)]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                r = __fadd_rn(r, lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)]);
+            const uint32_t dk = fresh ? ord32(r) : 0xFFFFFFFFu;
+            {
+                // prefetch the row of the likely next pop_min (smallest valid slot or fresh link)
+                const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
+                const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
+                uint32_t mk = dk < hL ? dk : hL;
+                mk = mk < hR ? mk : hR;
+                const int32_t mid = dk == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
+                const uint32_t mm = wave_min_u32(mk);
+                pred = -1;
+                if (mm != 0xFFFFFFFFu) {
+                    pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
+                    v1_pref = lane < deg0 ? a.nbr0[(size_t)pred * (size_t)deg0 + lane] : -1;
+                }
+            }
+            if (fresh) { // VisitedTable::advance list (stored after the loads above)
+                const int p = clear_n + __builtin_popcountll(fm & lanes_below(lane));
+                if (p < a.clear_cap)
+                    clr[p] = v1;
+            }
+            clear_n += nf;
+            DRM_FSTAMP(4);
+            // add_to_heap for each fresh link in row order
+            uint64_t rem = fm, accm = 0;
+            while (rem) {
+                const int l = __builtin_ctzll(rem);
+                rem &= rem - 1;
+                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
+                if (!LOGRES) {
+                    if (key < thr)
+                        add_result(pack(key, __builtin_amdgcn_readlane(v1, l)));
+                }
+                if (kc == ef) { // MinimaxHeap::push on a full heap
+                    if (key >= hi32(root))
+                        continue;
+                    if (lo32(root) != kPopLo)
+                        --nvalid;
+                    hp.pop(kc, lane);
+                    --kc;
+                }
+                ++kc;
+                hp.push(kc, pack(key, __builtin_amdgcn_readlane(v1, l)), lane);
+                ++nvalid;
+                root = readlane64(hp.R, 63);
+                accm |= 1ull << l;
+            }
+            if (LOGRES && accm) {
+                const int na = __builtin_popcountll(accm);
+                if (logn + na > a.log_cap) {
+                    // compact in place: the current result set (k entries) replaces the log
+                    const uint32_t T = hi32(root);
+                    const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
+                    logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
+                        __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }, lane);
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                if ((accm >> lane) & 1ull)
+                    __hip_atomic_store(lg + logn + __builtin_popcountll(accm & lanes_below(lane)), pack(dk, v1),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                logn += na;
+            }
+            nstep++;
+            DRM_FSTAMP(5);
+        }
+        DRM_FSTAMP(2);
+
+        // --- SingleResultHandler::end (heap_reorder): ascending (distance, id), (+inf, -1) padding
+        if (LOGRES) {
+            __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
+            __syncthreads();
+            const uint32_t T = kc == ef ? hi32(root) : 0xFFFFFFFFu;
+            const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
+            const int c = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) { stage[p] = e; }, lane);
+            __syncthreads();
+            {
+                uint64_t x0 = lane < c ? stage[lane] : ~0ull;
+                uint64_t x1 = lane + 64 < c ? stage[lane + 64] : ~0ull;
+                sort128(x0, x1, lane);
+                __syncthreads();
+                stage[lane] = x0;
+                stage[lane + 64] = x1;
+                __syncthreads();
+            }
+            for (int j = lane; j < k; j += 64) {
+                const int64_t o = (int64_t)q * k + j;
+                const uint64_t e = stage[j];
+                a.D[o] = j < c ? unord32(hi32(e)) : INFINITY;
+                a.I[o] = j < c ? (int64_t)unpack_id(e) : (int64_t)-1;
+            }
+            __syncthreads();
+        } else if (lane < k) {
+            const int64_t o = (int64_t)q * k + lane;
+            const bool valid = rv != ~0ull;
+            a.D[o] = valid ? unord32(hi32(rv)) : INFINITY;
+            a.I[o] = valid ? (int64_t)unpack_id(rv) : (int64_t)-1;
+        }
+        if (lane == 0) {
+            a.ndis[q] = ndis + ndis0;
+            a.nhops[q] = nhops + nstep;
+            if (a.nhops_upper)
+                a.nhops_upper[q] = nhops_upper;
+        }
+        // VisitedTable::advance: clear exactly the bits this query set
+        if (clear_n <= a.clear_cap) {
+            for (int t = lane; t < clear_n; t += 64)
+                vis[clr[t] >> 5] = 0u;
+        } else {
+            for (int64_t w = lane; w < a.vis_words; w += 64)
+                vis[w] = 0u;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        DRM_FSTAMP(6);
+    }
+    if (STAMPS && lane == 0 && a.stamps)
+        for (int i = 0; i < 12; ++i)
+            atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
+}
+
+} // namespace
+
+bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
+{
+    return ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8 && ix.deg0 <= 64 && efc <= 128 &&
+           (k == efc || k <= 64) && ix.vmode == 0;
+}
+
+void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream)
+{
+    const bool logres = a.k == a.ef;
+    if (logres) {
+        if (stamps)
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true>), dim3(slots), dim3(64), lds, stream, a);
+        else
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false>), dim3(slots), dim3(64), lds, stream, a);
+    } else {
+        if (stamps)
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true>), dim3(slots), dim3(64), lds, stream, a);
+        else
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false>), dim3(slots), dim3(64), lds, stream, a);
+    }
+    DRM_HIP_CHECK(hipGetLastError());
+}
+
+} // namespace drm

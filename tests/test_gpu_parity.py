@@ -172,6 +172,31 @@ def test_search_ties_fallback(repeats, k, ef, monkeypatch):
     assert 0 < nfb <= len(repeats["q"])
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
+@pytest.mark.parametrize("k,ef", [(128, 128), (64, 64), (5, 128), (16, 100), (100, 100), (32, 32)])
+def test_search_lean_and_exact_kernels_ties(repeats, k, ef, fast, monkeypatch):
+    """The lean kernel (hnsw_pq_fast.hip: packed-u64 pair heap, logged result set at k == ef,
+    register result set at k <= 64) and the general exact kernel (DRM_SEARCH_FAST=0) on the
+    tie-heavy index: both bit-identical to the oracle."""
+    monkeypatch.setenv("DRM_SEARCH_FAST", fast)
+    _search_both(repeats["index"], repeats["fx"], repeats["q"], k, ef)
+
+
+def test_search_lean_kernel_log_compaction(syn20k, repeats, monkeypatch):
+    """A log capacity just above ef forces the in-place compaction of the accepted-push log
+    (the result set is re-derived mid-walk) on most queries: still bit-identical."""
+    monkeypatch.setenv("DRM_SEARCH_LOG_CAP", "1")  # clamped to ef + 64
+    w = syn20k["w"]
+    _search_both(syn20k["index"], syn20k["fx"], w.q_emb[:600], 128, 128)
+    _search_both(repeats["index"], repeats["fx"], repeats["q"], 96, 96)
+
+
+def test_search_syn20k_exact_kernel(syn20k, monkeypatch):
+    monkeypatch.setenv("DRM_SEARCH_FAST", "0")
+    w = syn20k["w"]
+    _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
+
+
 def test_search_exact_kernel_forced(syn20k, monkeypatch):
     """DRM_SEARCH_SORTED=1 with DRM_SEARCH_EXACT=1 (read at index load): exact kernel only."""
     monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
