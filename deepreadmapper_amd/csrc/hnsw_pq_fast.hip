@@ -110,6 +110,58 @@ struct Heap {
             R = rootv;
     }
 
+    // heap_pop(128) on the full ef = 128 heap: the last slot (127) is lane 63's L. The max-child
+    // path is walked on the scalar unit over two ballots (which child each node takes, whether it
+    // moves up) -- a few SALU cycles per level instead of a chain of cross-lane round trips -- while
+    // the one ds_bpermute that fetches the moving values is already in flight.
+    __device__ __forceinline__ void pop128(int lane)
+    {
+        const uint64_t val = readlane64(L, 63);
+        const bool takeL = lane == 63 || L > R;
+        const int ch = takeL ? 2 * lane + 1 : 2 * lane + 2;
+        const uint64_t chv = takeL ? L : R;
+        const uint64_t up = bperm64(chv, ch & 63);
+        const uint64_t lm = ballot(takeL), mv = ballot(!(val > chv));
+        uint64_t W = 0;
+        uint32_t hole = 0;
+#pragma unroll
+        for (int d = 0; d < 7; ++d) {
+            if (hole >= 64u || !((mv >> hole) & 1ull))
+                break;
+            W |= 1ull << hole;
+            hole = 2u * hole + 2u - (uint32_t)((lm >> hole) & 1ull);
+        }
+        const bool writer = (W >> lane) & 1ull;
+        const uint64_t nv = (uint32_t)ch == hole ? val : up;
+        if (writer && takeL)
+            L = nv;
+        if (writer && !takeL)
+            R = nv;
+        const uint64_t rootv = (W & 1ull) ? readlane64(chv, 0) : val;
+        if (lane == 63)
+            R = rootv;
+    }
+
+    // heap_push(128, val) right after pop128: val enters at slot 127 (lane 63 L); its ancestors are
+    // slots 63, 31, 15, 7, 3, 1 (the L halves of lanes 31, 15, 7, 3, 1, 0) and the root (lane 63 R).
+    // Every holder compares its own ancestor with val in place; chain index m = 7 - bitlen(lane + 1)
+    // receives its father's value (m < h) or val (m == h), fetched by one ds_bpermute.
+    __device__ __forceinline__ void push128(uint64_t val, int lane)
+    {
+        const bool holderL = lane == 63 || (lane < 32 && ((lane + 1) & lane) == 0); // slots 127, 63, ..., 1
+        const bool anc = lane == 63 || holderL;                                    // ancestors: lane 63 is the root
+        const uint64_t av = lane == 63 ? R : L;
+        const int h = __builtin_popcountll(ballot(anc && val > av));
+        const uint64_t rootv = readlane64(R, 63);
+        const uint64_t fl = bperm64(L, lane >> 1);
+        const uint64_t srcv = lane == 0 ? rootv : fl;
+        const int m = 7 - bitlen((uint32_t)lane + 1u);
+        if (holderL && m <= h)
+            L = m < h ? srcv : val;
+        if (h == 7 && lane == 63)
+            R = val;
+    }
+
     // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
     __device__ __forceinline__ void push(int k, uint64_t val, int lane)
     {
@@ -406,8 +458,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             clear_n += nf;
             DRM_FSTAMP(4);
-            // add_to_heap for each fresh link in row order
+            // add_to_heap for each fresh link in row order. On a full heap the root distance only
+            // falls, so a link at or above it now is rejected for the whole row: it is skipped here.
             uint64_t rem = fm, accm = 0;
+            if (LOGRES && kc == ef)
+                rem &= ballot(dk < hi32(root));
             while (rem) {
                 const int l = __builtin_ctzll(rem);
                 rem &= rem - 1;
@@ -416,16 +471,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (key < thr)
                         add_result(pack(key, __builtin_amdgcn_readlane(v1, l)));
                 }
-                if (kc == ef) { // MinimaxHeap::push on a full heap
+                const uint64_t val = pack(key, __builtin_amdgcn_readlane(v1, l));
+                if (kc == ef) { // MinimaxHeap::push on a full heap: pop the max, push val
                     if (key >= hi32(root))
                         continue;
                     if (lo32(root) != kPopLo)
                         --nvalid;
-                    hp.pop(kc, lane);
-                    --kc;
+                    if (ef == 128) {
+                        hp.pop128(lane);
+                        hp.push128(val, lane);
+                    } else {
+                        hp.pop(kc, lane);
+                        hp.push(kc, val, lane);
+                    }
+                } else {
+                    ++kc;
+                    hp.push(kc, val, lane);
                 }
-                ++kc;
-                hp.push(kc, pack(key, __builtin_amdgcn_readlane(v1, l)), lane);
                 ++nvalid;
                 root = readlane64(hp.R, 63);
                 accm |= 1ull << l;

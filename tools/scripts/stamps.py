@@ -1,5 +1,6 @@
-"""Diagnostic: section time shares of the search kernel (stamped build, DRM_SEARCH_STAMPS=1).
-Run on the GPU box after the bench cache exists: DRM_SEARCH_STAMPS=1 python tools/scripts/stamps.py"""
+"""Diagnostic: section time shares of the HNSW-PQ search kernel (stamped build, DRM_SEARCH_STAMPS=1).
+Run on the GPU box after the bench cache exists: DRM_SEARCH_STAMPS=1 python tools/scripts/stamps.py
+(DRM_SEARCH_FAST=0 stamps the general exact kernel instead of the lean one)."""
 import ctypes as C
 import os
 import sys
@@ -23,9 +24,13 @@ out = np.zeros(12, dtype=np.uint64)
 L = lib()
 L.drm_debug_search_stamps.argtypes = [C.c_void_p, C.c_void_p]
 check(L.drm_debug_search_stamps(ix.handle, out.ctypes.data))
-names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances+prefetch",
-         "push loop: fetch/reject/overhead", "output+clear", "queue/top", "push loop: add_result",
-         "push loop: evict (heap_pop)", "push loop: heap_push", "-"]
+if os.environ.get("DRM_SEARCH_FAST", "1") != "0":
+    names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+codes)", "distances+prefetch+clear list",
+             "push loop (+log store)", "output+clear", "queue/top", "-", "-", "-", "-"]
+else:
+    names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances+prefetch",
+             "push loop: fetch/reject/overhead", "output+clear", "queue/top", "push loop: add_result",
+             "push loop: evict (heap_pop)", "push loop: heap_push", "-"]
 tot = float(out.sum())
 for n, v in zip(names, out):
-    print(f"{n:28s} {v / tot * 100:6.2f} %")
+    print(f"{n:32s} {v / tot * 100:6.2f} %")
