@@ -27,7 +27,8 @@ EXPORTS = [
     "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device",
     "drm_search_device_ex", "drm_search_fallbacks", "drm_sw_scores",
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
-    "drm_build_hnswpq", "drm_build_hnsw_flat", "drm_embed_kmer3",
+    "drm_build_hnswpq", "drm_build_hnsw_flat", "drm_embed_kmer3", "drm_build_hnswpq_device",
+    "drm_embed_kmer3_device",
     "drm_flat_index_load", "drm_flat_index_free", "drm_flat_index_get_info", "drm_flat_search",
     "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_fallbacks",
 ]
@@ -114,6 +115,9 @@ def lib():
         "drm_flat_search_fallbacks": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_build_hnsw_flat": (C.c_int, [vp, i64, i32, i32, i32, i32, C.c_uint64, C.c_char_p]),
         "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),
+        "drm_build_hnswpq_device": (C.c_int, [vp, i64, i32, i32, i32, i32, i32, C.c_double, C.c_uint64, C.c_int,
+                                              C.c_char_p]),
+        "drm_embed_kmer3_device": (C.c_int, [vp, i64, i32, i64, i32, C.c_uint64, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

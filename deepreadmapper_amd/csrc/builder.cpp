@@ -288,6 +288,67 @@ struct Builder {
 
 } // namespace
 
+std::vector<size_t> pq_training_rows(int64_t n, double sample_rate, int ksub, uint64_t seed)
+{
+    // create_training_set (src/hnswpq/index.cpp:57-84): evenly spaced, n_train = n * sample_rate
+    size_t n_train = (size_t)((double)n * sample_rate);
+    if (n_train < 1)
+        n_train = 1;
+    const double step = (double)n / (double)n_train;
+    // faiss Clustering subsamples to max_points_per_centroid (256) * k points
+    const size_t n_fit = std::min(n_train, (size_t)256 * ksub);
+    std::vector<size_t> idx(n_train);
+    for (size_t i = 0; i < n_train; ++i)
+        idx[i] = std::min((size_t)((double)i * step), (size_t)n - 1);
+    if (n_fit < n_train) {
+        std::mt19937 rng((uint32_t)(seed * 2654435761u + 1234));
+        for (size_t i = 0; i < n_fit; ++i)
+            std::swap(idx[i], idx[i + rng() % (n_train - i)]);
+        idx.resize(n_fit);
+    }
+    return idx;
+}
+
+void pq_train_subspaces(const float *rows, size_t n_fit, int d, int M, int nbits, uint64_t seed, int nthreads,
+                        float *centroids)
+{
+    const int dsub = d / M, ksub = 1 << nbits;
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+    std::vector<float> sub(n_fit * (size_t)dsub);
+    for (int m = 0; m < M; ++m) {
+        for (size_t i = 0; i < n_fit; ++i)
+            std::memcpy(&sub[i * dsub], rows + i * d + (size_t)m * dsub, sizeof(float) * dsub);
+        kmeans(sub.data(), n_fit, dsub, ksub, 25, seed + 1234 + (uint64_t)m, centroids + (size_t)m * ksub * dsub,
+               nthreads);
+    }
+}
+
+int hnsw_assign_levels(HnswPqHost &ix, int64_t n, int M_hnsw, uint64_t seed)
+{
+    // HNSW(M): default probas, levels ~ random_level() [faiss HNSW::prepare_level_tab]
+    hnsw_default_probas(M_hnsw, ix.assign_probas, ix.cum_nneighbor_per_level);
+    std::mt19937 lrng((uint32_t)(12345 + seed));
+    ix.levels.resize((size_t)n);
+    ix.offsets.assign((size_t)n + 1, 0);
+    int top_level = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        double f = lrng() / double(lrng.max());
+        int level = (int)ix.assign_probas.size() - 1;
+        for (int l = 0; l < (int)ix.assign_probas.size(); ++l) {
+            if (f < ix.assign_probas[l]) {
+                level = l;
+                break;
+            }
+            f -= ix.assign_probas[l];
+        }
+        ix.levels[i] = level + 1;
+        top_level = std::max(top_level, level);
+        ix.offsets[i + 1] = ix.offsets[i] + (uint64_t)ix.cum_nneighbor_per_level[level + 1];
+    }
+    return top_level;
+}
+
 void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_hnsw, int efc, double sample_rate,
                   int nthreads, uint64_t seed, const std::string &path)
 {
@@ -309,28 +370,12 @@ void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_h
     pq.code_size = (M_pq * nbits + 7) / 8;
     pq.centroids.resize((size_t)d * pq.ksub);
 
-    // create_training_set (src/hnswpq/index.cpp:57-84): evenly spaced, n_train = n * sample_rate
-    size_t n_train = (size_t)((double)n * sample_rate);
-    if (n_train < 1)
-        n_train = 1;
-    double step = (double)n / (double)n_train;
-    // faiss Clustering subsamples to max_points_per_centroid (256) * k points
-    size_t n_fit = std::min(n_train, (size_t)256 * pq.ksub);
-    std::vector<size_t> train_idx(n_train);
-    for (size_t i = 0; i < n_train; ++i)
-        train_idx[i] = std::min((size_t)((double)i * step), (size_t)n - 1);
-    if (n_fit < n_train) {
-        std::mt19937 rng((uint32_t)(seed * 2654435761u + 1234));
-        for (size_t i = 0; i < n_fit; ++i)
-            std::swap(train_idx[i], train_idx[i + rng() % (n_train - i)]);
-        train_idx.resize(n_fit);
-    }
-    std::vector<float> sub((size_t)train_idx.size() * pq.dsub);
-    for (int m = 0; m < M_pq; ++m) {
-        for (size_t i = 0; i < train_idx.size(); ++i)
-            std::memcpy(&sub[i * pq.dsub], x + train_idx[i] * d + (size_t)m * pq.dsub, sizeof(float) * pq.dsub);
-        kmeans(sub.data(), train_idx.size(), pq.dsub, pq.ksub, 25, seed + 1234 + (uint64_t)m,
-               pq.centroids.data() + (size_t)m * pq.ksub * pq.dsub, nthreads);
+    {
+        const std::vector<size_t> rows = pq_training_rows(n, sample_rate, pq.ksub, seed);
+        std::vector<float> tx(rows.size() * (size_t)d);
+        for (size_t i = 0; i < rows.size(); ++i)
+            std::memcpy(&tx[i * d], x + rows[i] * d, sizeof(float) * d);
+        pq_train_subspaces(tx.data(), rows.size(), d, M_pq, nbits, seed, nthreads, pq.centroids.data());
     }
     pq.sdc.resize((size_t)M_pq * pq.ksub * pq.ksub);
     for (int m = 0; m < M_pq; ++m)
@@ -353,28 +398,9 @@ void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_h
     for (int64_t i = 0; i < n; ++i)
         pq.encode(x + (size_t)i * d, ix.codes.data() + (size_t)i * pq.code_size);
 
-    // HNSW(M): default probas, levels ~ random_level() [faiss HNSW::prepare_level_tab]
-    hnsw_default_probas(M_hnsw, ix.assign_probas, ix.cum_nneighbor_per_level);
     ix.efConstruction = efc;
     ix.efSearch = 16;
-    std::mt19937 lrng((uint32_t)(12345 + seed));
-    ix.levels.resize((size_t)n);
-    ix.offsets.assign((size_t)n + 1, 0);
-    int top_level = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        double f = lrng() / double(lrng.max());
-        int level = (int)ix.assign_probas.size() - 1;
-        for (int l = 0; l < (int)ix.assign_probas.size(); ++l) {
-            if (f < ix.assign_probas[l]) {
-                level = l;
-                break;
-            }
-            f -= ix.assign_probas[l];
-        }
-        ix.levels[i] = level + 1;
-        top_level = std::max(top_level, level);
-        ix.offsets[i + 1] = ix.offsets[i] + (uint64_t)ix.cum_nneighbor_per_level[level + 1];
-    }
+    const int top_level = hnsw_assign_levels(ix, n, M_hnsw, seed);
     ix.neighbors.assign(ix.offsets.back(), -1);
 
     Builder B(ix, pq);

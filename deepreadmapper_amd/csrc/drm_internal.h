@@ -121,8 +121,23 @@ std::string read_whole_file(const std::string &path);
 
 void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_hnsw, int efc, double sample_rate,
                   int nthreads, uint64_t seed, const std::string &path);
+// Shared by the CPU builder (builder.cpp) and the GPU builder (builder_gpu.hip):
+// create_training_set's evenly spaced rows (src/hnswpq/index.cpp:57-84), subsampled to 256 * ksub;
+std::vector<size_t> pq_training_rows(int64_t n, double sample_rate, int ksub, uint64_t seed);
+// k-means (25 iterations) per sub-quantizer on rows [n_fit][d] -> centroids [M][2^nbits][d / M];
+void pq_train_subspaces(const float *rows, size_t n_fit, int d, int M, int nbits, uint64_t seed, int nthreads,
+                        float *centroids);
+// HNSW::set_default_probas + random_level for n nodes: fills assign_probas, cum_nneighbor_per_level,
+// levels (level + 1) and offsets of ix; returns the top level.
+int hnsw_assign_levels(HnswPqHost &ix, int64_t n, int M_hnsw, uint64_t seed);
+// GPU construction (builder_gpu.hip) from device-resident vectors d_x [n][d]: same file layout and
+// levels as build_hnswpq, PQ trained on the host, codes and graph built on `device`.
+void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, int M_hnsw, int efc,
+                      double sample_rate, uint64_t seed, int device, const std::string &path);
 void embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len, int64_t n, int dim, uint64_t seed,
                  float *out);
+// the [64 x dim] N(0,1) projection of the stand-in embedder (splitmix64(seed) + Box-Muller)
+std::vector<double> kmer3_matrix(int dim, uint64_t seed);
 constexpr uint64_t kEmbedSeed = 42; // seed of the stand-in embedder used by the CLIs
 
 } // namespace drm

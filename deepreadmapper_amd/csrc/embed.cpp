@@ -17,7 +17,7 @@ static inline uint64_t splitmix64(uint64_t &s)
     return z ^ (z >> 31);
 }
 
-static std::vector<double> kmer3_matrix(int dim, uint64_t seed)
+std::vector<double> kmer3_matrix(int dim, uint64_t seed)
 {
     std::vector<double> R((size_t)64 * dim);
     uint64_t s = seed;

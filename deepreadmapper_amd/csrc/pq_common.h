@@ -172,9 +172,8 @@ __device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float 
 // set_query for the lean kernel (M = 8, ksub = 256, dsub = 16, 16-B aligned queries): the same
 // per-entry op order as build_lut, with the query sub-vector made wave-uniform (SGPRs) so that only
 // the two centroids a lane works on occupy VGPRs (32 of them).
-__device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, float *lut, int lane)
+__device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *centroids, float *lut, int lane)
 {
-    const float *qv = a.x + q * a.d;
     for (int m = 0; m < 8; ++m) {
         float xs[16];
 #pragma unroll
@@ -188,8 +187,8 @@ __device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, flo
 #pragma unroll 1
         for (int c0 = 0; c0 < 256; c0 += 128) {
             const int e0 = m * 256 + c0 + lane;
-            const float4 *ca = reinterpret_cast<const float4 *>(a.centroids + (size_t)e0 * 16);
-            const float4 *cb = reinterpret_cast<const float4 *>(a.centroids + (size_t)(e0 + 64) * 16);
+            const float4 *ca = reinterpret_cast<const float4 *>(centroids + (size_t)e0 * 16);
+            const float4 *cb = reinterpret_cast<const float4 *>(centroids + (size_t)(e0 + 64) * 16);
             float4 u[4], w[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -214,6 +213,10 @@ __device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, flo
         }
     }
     __syncthreads();
+}
+__device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, float *lut, int lane)
+{
+    build_lut_m8_ptr(a.x + q * a.d, a.centroids, lut, lane);
 }
 
 // greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss]

@@ -103,6 +103,31 @@ def build_index(x, path, M_pq=8, nbits=8, M_hnsw=16, efc=200, sample_rate=0.5, n
                                  C.c_uint64(seed), str(path).encode()))
 
 
+def build_index_gpu_from_rows(rows, path, M_pq=8, nbits=8, M_hnsw=16, efc=200, sample_rate=0.5, seed=0, device=0,
+                              log=None):
+    """GPU build (drm_build_hnswpq_device) over the stand-in embeddings of fixed-length rows (e.g. the
+    window table): the rows are embedded on the device (drm_embed_kmer3_device) and never leave it."""
+    from .device import DeviceBuffer, set_device, synchronize
+    import time
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    n, L = rows.shape
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    set_device(device)
+    t0 = time.time()
+    d_rows = DeviceBuffer.from_host(rows)
+    d_x = DeviceBuffer((n, 128), np.float32)
+    check(lib().drm_embed_kmer3_device(d_rows.ptr, n, L, L, 128, C.c_uint64(EMBED_SEED), d_x.ptr, None))
+    d_rows.free()
+    if log:
+        log(f"[synth] embedded {n} rows on the GPU in {time.time() - t0:.1f}s")
+    check(lib().drm_build_hnswpq_device(d_x.ptr, n, 128, M_pq, nbits, M_hnsw, efc, sample_rate, C.c_uint64(seed),
+                                        device, str(path).encode()))
+    synchronize()
+    d_x.free()
+    if log:
+        log(f"[synth] GPU-built IndexHNSWPQ over {n} vectors in {time.time() - t0:.1f}s")
+
+
 def build_flat_index(x, path, M=64, efc=128, nthreads=0, seed=0):
     """hnswlib build_index back end (src/hnswlib_dir/index.cpp:3-49) -> hnswlib file (fp32 L2)."""
     x = np.ascontiguousarray(x, dtype=np.float32)
@@ -134,8 +159,10 @@ class Workload:
         self.ref_len, self.stride, self.seed, self.read_seed, self.sub_rate = ref_len, stride, seed, read_seed, sub_rate
 
     def generate(self, workdir, efc=200, M_hnsw=16, M_pq=8, nbits=8, nthreads=0, build_seed=0, log=None,
-                 need_refs=True):
-        """need_refs=False skips the stride-1 window table (search-only workloads such as C4)."""
+                 need_refs=True, gpu_build=False, device=0):
+        """need_refs=False skips the stride-1 window table (search-only workloads such as C4).
+        gpu_build=True embeds the windows and builds the index on the GPU (builder_gpu.hip); the file
+        name carries a _gpu suffix so host- and GPU-built indexes never mix."""
         os.makedirs(workdir, exist_ok=True)
         self.genome = genome(self.genome_len, self.seed)
         # static ref_seqs: stride 1 always
@@ -144,7 +171,14 @@ class Workload:
                                                             self.sub_rate, self.read_seed)
         self.queries = tag(self.reads)
         self.q_emb = embed(self.queries)
-        self.index_path = os.path.join(workdir, f"{self.name}_M{M_hnsw}_efc{efc}_s{self.stride}.index")
+        suffix = "_gpu" if gpu_build else ""
+        self.index_path = os.path.join(workdir, f"{self.name}_M{M_hnsw}_efc{efc}_s{self.stride}{suffix}.index")
+        if not os.path.exists(self.index_path) and gpu_build:
+            base = windows_lookup(self.genome, self.ref_len, self.stride) if (self.refs is None or self.stride != 1) \
+                else self.refs
+            tmp = self.index_path + ".tmp"
+            build_index_gpu_from_rows(base, tmp, M_pq, nbits, M_hnsw, efc, 0.5, build_seed, device, log)
+            os.replace(tmp, self.index_path)
         if not os.path.exists(self.index_path):
             base = windows_lookup(self.genome, self.ref_len, self.stride)
             if log:

@@ -187,6 +187,15 @@ int drm_build_hnswpq(const float *x, int64_t n, int32_t d, int32_t M_pq, int32_t
                      int32_t efConstruction, double sample_rate, int32_t nthreads, uint64_t seed,
                      const char *index_path);
 
+/* The same build on one GPU (builder_gpu.hip), from DEVICE-resident vectors d_x [n x d] f32 (d = 128,
+ * M_pq = 8, nbits = 8): PQ trained on the host on the same sample as drm_build_hnswpq, codes and the
+ * graph built on `device` (batched insertion, ef = min(efConstruction, 256) beams, closest-first
+ * neighbour selection), written as the same faiss "IHNp" file. For the 10M-50M synthetic configurations
+ * (BASELINE.json configs[3..4]) that the host builder cannot produce inside a run. */
+int drm_build_hnswpq_device(const float *d_x, int64_t n, int32_t d, int32_t M_pq, int32_t nbits, int32_t M_hnsw,
+                            int32_t efConstruction, double sample_rate, uint64_t seed, int device,
+                            const char *index_path);
+
 /* build_index (src/hnswlib_dir/index.cpp:3-49): hnswlib HierarchicalNSW<float>(L2Space(d), n, M,
  * efConstruction), addPoint(x[i], label i) for all i, saveIndex -> an hnswlib file (the reference's
  * defaults: M = Config::Build::GPH_DEG = 64, EFC = 128, includes/utils/config.hpp:30-31). The graph
@@ -201,6 +210,11 @@ int drm_build_hnsw_flat(const float *x, int64_t n, int32_t d, int32_t M, int32_t
  * that reads land near their source windows. seqs: n strings at seqs[off[i] .. +len[i]). */
 int drm_embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len, int64_t n, int32_t dim,
                     uint64_t seed, float *out);
+
+/* drm_embed_kmer3 on the device for n fixed-length rows (d_rows[i * row_stride .. + len), len <= 512,
+ * dim = 128), enqueued on `stream` and synchronised; bit-identical to drm_embed_kmer3. */
+int drm_embed_kmer3_device(const uint8_t *d_rows, int64_t n, int32_t len, int64_t row_stride, int32_t dim,
+                           uint64_t seed, float *d_out, void *stream);
 
 #ifdef __cplusplus
 }

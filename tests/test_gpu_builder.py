@@ -1,0 +1,114 @@
+"""GPU index builder (builder_gpu.hip) and the device embedder.
+
+* drm_embed_kmer3_device is bit-identical to the host embedder (fp64 sums in the host's order);
+* the GPU-built file is a valid faiss IHNp that the reader, the oracle and the HIP search accept, with
+  the host builder's PQ codebook, codes, levels and entry point (same sample, same RNG), and the HIP
+  search on it is bit-identical to the oracle on it;
+* its graph is a different (closest-first, batched) HNSW: its recall of the true source window must
+  stay close to the host-built graph's on the same reads."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _embed_device(rows):
+    import ctypes as C
+    from deepreadmapper_amd._native import check, lib
+    from deepreadmapper_amd.device import DeviceBuffer
+    from deepreadmapper_amd.synth import EMBED_SEED
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    d_rows = DeviceBuffer.from_host(rows)
+    d_x = DeviceBuffer((rows.shape[0], 128), np.float32)
+    check(lib().drm_embed_kmer3_device(d_rows.ptr, rows.shape[0], rows.shape[1], rows.shape[1], 128,
+                                       C.c_uint64(EMBED_SEED), d_x.ptr, None))
+    return d_x.download()
+
+
+def test_embed_device_bitexact():
+    from deepreadmapper_amd import synth
+    rng = np.random.default_rng(5)
+    rows = synth.ACGT[rng.integers(0, 4, size=(5003, 152))]
+    rows[::7, 40] = ord("N")          # non-ACGT bytes break 3-mers, as on the host
+    rows[::11, :] = ord("N")          # an all-N row embeds to zeros
+    rows[:, 0], rows[:, -1] = ord("<"), ord(">")
+    assert np.array_equal(_embed_device(rows).view(np.uint32), synth.embed(rows).view(np.uint32))
+
+
+def _build_both(tmp_path, rows, name):
+    from deepreadmapper_amd import synth
+    x = synth.embed(rows)
+    host = str(tmp_path / f"{name}_host.index")
+    gpu = str(tmp_path / f"{name}_gpu.index")
+    synth.build_index(x, host, nthreads=1)
+    synth.build_index_gpu_from_rows(rows, gpu)
+    return x, host, gpu
+
+
+def test_gpu_build_c1_layout_and_search_parity(tmp_path, c1):
+    from oracle import faiss_file
+    from deepreadmapper_amd import read_index
+    x, host, gpu = _build_both(tmp_path, c1["refs"], "c1")
+    fh, fg = faiss_file.read(host), faiss_file.read(gpu)
+    assert fg.ntotal == fh.ntotal == 1702 and fg.d == 128
+    assert np.array_equal(fg.centroids, fh.centroids)   # same training sample, same k-means
+    assert np.array_equal(fg.codes, fh.codes)           # same encoder op order on the GPU
+    assert np.array_equal(fg.levels, fh.levels) and np.array_equal(fg.offsets, fh.offsets)
+    assert fg.entry_point == fh.entry_point and fg.max_level == fh.max_level
+    # every list: valid ids first, no self links, no duplicates
+    for i in range(fg.ntotal):
+        row = fg.neighbors[fg.offsets[i]:fg.offsets[i + 1]]
+        for l in range(fg.levels[i]):
+            seg = row[fg.cum_nneighbor_per_level[l]:fg.cum_nneighbor_per_level[l + 1]]
+            v = seg[seg >= 0]
+            assert (seg[:len(v)] >= 0).all() and i not in v and len(set(v.tolist())) == len(v)
+            assert (fg.levels[v] > l).all()
+    ix = read_index(gpu)
+    D, I, st = ix.search(c1["q"], 128, 128)
+    ix.free()
+    Do, Io, nd, nh = O.hnswpq_search(fg, c1["q"], 128, 128)
+    assert np.array_equal(I, Io) and np.array_equal(D.view(np.uint32), Do.view(np.uint32))
+    assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+
+
+def test_gpu_build_recall_vs_host(tmp_path):
+    """20k windows + 2000 simulated reads: the source window's rank in the search results."""
+    from deepreadmapper_amd import synth, read_index
+    g = synth.genome(10_149, seed=5)
+    refs = synth.windows_lookup(g, 150, 1)
+    reads, _, truth = synth.simulate_reads(g, 2000, seed=11)
+    q = synth.embed(synth.tag(reads))
+    x, host, gpu = _build_both(tmp_path, synth.tag(refs), "syn")
+    rec = {}
+    for name, path in (("host", host), ("gpu", gpu)):
+        ix = read_index(path)
+        _, I, _ = ix.search(q, 128, 128)
+        ix.free()
+        rec[name] = float(np.mean((I == truth[:, None]).any(axis=1)))
+    print("truth-in-top-128 recall", rec)
+    assert rec["gpu"] >= 0.9 * rec["host"]
+
+
+def test_gpu_build_c3_scale(tmp_path):
+    """C3 size (1M windows): the GPU build finishes in seconds and its recall on 5k reads stays close
+    to the host-built C3 index's (built here too)."""
+    from deepreadmapper_amd import synth, read_index
+    w = synth.Workload("c3g", 500_149, 5000, seed=42, read_seed=7)
+    t0 = time.time()
+    w.generate(str(tmp_path), gpu_build=True)
+    t_gpu = time.time() - t0
+    host = synth.Workload("c3h", 500_149, 5000, seed=42, read_seed=7).generate(
+        str(tmp_path), nthreads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    rec = {}
+    for name, path in (("host", host.index_path), ("gpu", w.index_path)):
+        ix = read_index(path)
+        _, I, _ = ix.search(w.q_emb, 128, 128)
+        ix.free()
+        rec[name] = float(np.mean((I == w.truth[:, None]).any(axis=1)))
+    print(f"C3 GPU build {t_gpu:.1f}s (incl. embedding + file write); recall {rec}")
+    assert rec["gpu"] >= 0.9 * rec["host"]
