@@ -15,15 +15,15 @@
 //      builds its PQ LUT, descends greedily through the levels above its own, and on each of its levels
 //      runs an ef-bounded best-first beam (efConstruction, <= 256 in registers) over the nodes already
 //      inserted (ADC distances, per-slot visited bitmap as in the search kernel); it links to the
-//      closest degree-many candidates. A second kernel adds the reverse links: each target list keeps
+//      candidates the neighbour heuristic keeps (below). A second kernel adds the reverse links: each target list keeps
 //      its degree-many closest entries (one 64-bit CAS on the (distance, id) pair that is the current
 //      maximum; retried on conflict). Neighbours of one batch do not see each other; the growing
 //      batches keep that effect small, as in other batched GPU HNSW builders;
 //   5. lists sorted by distance, packed into faiss's offsets/neighbors layout, file written on the host.
-// Selection is "closest first" rather than faiss's shrink_neighbor_list heuristic: the heuristic's
-// pairwise PQ distances between candidates (up to efC x degree symmetric distances per insertion) cost
-// more than the rest of the build on the GPU. The graph is therefore not faiss's graph; the file
-// format, levels, entry point and PQ are.
+// Forward links follow faiss's shrink_neighbor_list heuristic with symmetric PQ distances (sdc_table),
+// applied to the 64 nearest candidates (faiss scans all efC); reverse links keep the closest entries
+// instead of re-running the heuristic on the target's list. The graph is therefore not faiss's graph;
+// the file format, levels, entry point and PQ are.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -94,6 +94,7 @@ struct BuildArgs {
     int32_t d;
     const float *centroids;
     const uint8_t *codes;
+    const float *sdc;    // [M][256][256] symmetric sub-distances (PQ sdc_table)
     uint64_t *link0;     // [n][deg0] packed (ord32(dist) << 32 | id), ~0 = empty
     uint64_t *linkU;     // level l >= 1 list of node i at uoff[i] + (l - 1) * degU
     const int64_t *uoff; // [n], -1 for level-0-only nodes
@@ -273,10 +274,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
                             W[r] = ~0ull;
                 }
             }
-            // forward links: the deg closest candidates (W[0 .. deg)); deg <= 64
+            // HNSW::shrink_neighbor_list over the 64 nearest candidates: candidate c (lane c, in distance
+            // order) is kept unless an already kept k is closer to it than the new node is
+            // (symmetric PQ distance sdc(k, c) < d(q, c)); at most deg are kept.
+            const bool has = W[0] != ~0ull;
+            const int32_t cid = has ? (int32_t)(uint32_t)W[0] : 0;
+            const uint2 cc = has ? *reinterpret_cast<const uint2 *>(a.codes + (size_t)cid * 8) : make_uint2(0u, 0u);
+            const float dq = unord32((uint32_t)(W[0] >> 32));
+            const int T = __builtin_popcountll(bballot(has));
+            uint64_t dom = 0;
+#pragma unroll 4
+            for (int k = 0; k + 1 < T; ++k) {
+                const uint32_t kx = (uint32_t)__builtin_amdgcn_readlane((int)cc.x, k);
+                const uint32_t ky = (uint32_t)__builtin_amdgcn_readlane((int)cc.y, k);
+                if (k < lane && has) {
+                    float sd = 0.0f;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        sd = __fadd_rn(sd, a.sdc[((m * 256 + ((kx >> (8 * m)) & 255u)) << 8) + ((cc.x >> (8 * m)) & 255u)]);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        sd = __fadd_rn(sd, a.sdc[(((m + 4) * 256 + ((ky >> (8 * m)) & 255u)) << 8) +
+                                                 ((cc.y >> (8 * m)) & 255u)]);
+                    if (sd < dq)
+                        dom |= 1ull << k;
+                }
+            }
+            uint64_t kept = 0;
+            int nk = 0;
+            for (int c = 0; c < T && nk < deg; ++c) {
+                const uint64_t dc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(dom >> 32), c) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)dom, c);
+                if ((dc & kept) == 0) {
+                    kept |= 1ull << c;
+                    ++nk;
+                }
+            }
+            // forward links: the kept candidates in distance order, then empty slots
             uint64_t *mine = l == 0 ? a.link0 + (size_t)u * a.deg0 : a.linkU + a.uoff[u] + (int64_t)(l - 1) * a.degU;
-            if (lane < deg)
-                mine[lane] = W[0];
+            if ((kept >> lane) & 1ull)
+                mine[__builtin_popcountll(kept & lanes_below(lane))] = W[0];
+            if (lane >= nk && lane < deg)
+                mine[lane] = ~0ull;
             // the next level starts from the nearest candidate found here
             cur = (int32_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)W[0], 0);
             dcur = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(W[0] >> 32), 0);
@@ -417,6 +456,22 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
     }
     if (verbose)
         std::fprintf(stderr, "[gpu build] PQ trained %.1fs\n", secs_since(t0));
+    // PQ sdc_table [M][ksub][ksub] (ProductQuantizer::compute_sdc_table), for the neighbour heuristic
+    std::vector<float> sdc((size_t)M_pq * ksub * ksub);
+    for (int m = 0; m < M_pq; ++m)
+        for (int i = 0; i < ksub; ++i)
+            for (int j = 0; j < ksub; ++j) {
+                const float *ci = &ix.centroids[((size_t)m * ksub + i) * dsub];
+                const float *cj = &ix.centroids[((size_t)m * ksub + j) * dsub];
+                float acc = 0.f;
+                for (int t = 0; t < dsub; ++t) {
+                    const float df = ci[t] - cj[t];
+                    acc += df * df;
+                }
+                sdc[((size_t)m * ksub + i) * ksub + j] = acc;
+            }
+    DevArr<float> dsdc(sdc.size());
+    DRM_HIP_CHECK(hipMemcpy(dsdc.p, sdc.data(), sizeof(float) * sdc.size(), hipMemcpyHostToDevice));
     DevArr<float> dcent(ix.centroids.size());
     DRM_HIP_CHECK(hipMemcpy(dcent.p, ix.centroids.data(), sizeof(float) * ix.centroids.size(), hipMemcpyHostToDevice));
     // 2. codes
@@ -479,6 +534,7 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
     a.d = d;
     a.centroids = dcent.p;
     a.codes = dcodes.p;
+    a.sdc = dsdc.p;
     a.link0 = dl0.p;
     a.linkU = dlu.p;
     a.uoff = duoff.p;
