@@ -119,7 +119,7 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=False):
+def cpu_baseline(refs, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=False):
     """Oracle (C / C++ restatement, OpenMP over queries) on a bounded sample of this workload."""
     from oracle import faiss_file, hnswlib_file, oracle as O
     from deepreadmapper_amd.rerank import pack_queries
@@ -129,8 +129,6 @@ def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=Fa
         fx = hnswlib_file.read(index_path)
     else:
         s = O.make_index(faiss_file.read(index_path))
-    refs = w.refs
-
     def run(n):
         q = q_emb[:n]
         t0 = time.perf_counter()
@@ -150,8 +148,71 @@ def cpu_baseline(w, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=Fa
     ts, tw = run(n)
     log_fn(f"[cpu] oracle on {n} queries x {threads} threads: search {ts:.2f}s, SW {tw:.2f}s")
     return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of this rank's C3 reads (oracle/ C restatement, OpenMP {threads} threads on "
+            "sample": f"first {n} of this rank's reads (oracle/ C restatement, OpenMP {threads} threads on "
                       f"{cpu_model()}): search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+
+
+def prepare_c3(args, D, dev):
+    """C3 (BASELINE.json configs[2]): a seeded 500,149 bp genome, stride-1 window
+    table of 1,000,000 fwd/RC windows, IndexHNSWPQ built by the host builder, 100k reads per GPU."""
+    from deepreadmapper_amd import synth
+    from deepreadmapper_amd.shard import shard_range
+    N, Q = D.world, args.queries or 100_000
+    w = synth.Workload("c3", 500_149, N * Q, seed=42, read_seed=7)
+    # rank 0 builds the shared index file; the others wait, then every rank loads its own replica
+    if D.rank == 0:
+        t0 = time.time()
+        w.generate(args.cache, nthreads=args.build_threads, log=log)
+        log(f"[bench] workload ready in {time.time() - t0:.1f}s: {len(w.refs)} windows, index {w.index_path}")
+    D.barrier()
+    if D.rank != 0:
+        w.generate(args.cache)
+    lo, hi = shard_range(N * Q, D.rank, N)  # contiguous query shard of this rank
+    return {"Q": Q, "refs": w.refs, "index_path": w.index_path, "q_emb": np.ascontiguousarray(w.q_emb[lo:hi]),
+            "queries": np.ascontiguousarray(w.queries[lo:hi]), "truth": w.truth[lo:hi],
+            "desc": "C3: synthetic 1M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200), search + SW "
+                    "rerank, EF=128 K=128"}
+
+
+C5_GENOME = 25_000_149  # 2 * (L - 149) = 50,000,000 stride-1 windows
+
+
+def prepare_c5(args, D, dev):
+    """C5 per-GPU slice (BASELINE.json configs[4], the configuration the 1/2/4/8-GPU
+    metric is quoted on): a seeded 25,000,149 bp genome, stride-1 window table of 50,000,000 fwd/RC
+    150 bp windows, an IndexHNSWPQ (M_pq 8, nbits 8, M_hnsw 16, EFC 200) over them built on the GPU
+    (builder_gpu.hip) and replicated on every GPU, and 1.25M reads per GPU (weak scaling: rank r takes
+    reads [r*Q, (r+1)*Q) of one seeded read stream, so the 8-GPU job searches 10M reads). Rank 0
+    writes the window table and the index once; every rank memory-maps the table and loads the file."""
+    from deepreadmapper_amd import synth
+    N, Q = D.world, args.queries or 1_250_000
+    os.makedirs(args.cache, exist_ok=True)
+    g = synth.genome(C5_GENOME, seed=44)
+    n_ref = 2 * (C5_GENOME - 149)
+    refs_path = os.path.join(args.cache, "c5_refs_150.u8")
+    index_path = os.path.join(args.cache, "c5_M16_efc200_s1_gpu.index")
+    if D.rank == 0:
+        t0 = time.time()
+        if not os.path.exists(refs_path):
+            synth.windows_lookup(g, 150, 1).tofile(refs_path + ".tmp")
+            os.replace(refs_path + ".tmp", refs_path)
+            log(f"[bench] C5 window table ({n_ref} windows) written in {time.time() - t0:.1f}s")
+        if not os.path.exists(index_path):
+            rows = np.memmap(refs_path, dtype=np.uint8, mode="r", shape=(n_ref, 150))
+            synth.build_index_gpu_from_rows(rows, index_path + ".tmp", device=dev, log=log)
+            os.replace(index_path + ".tmp", index_path)
+            del rows
+        log(f"[bench] C5 workload ready in {time.time() - t0:.1f}s")
+    D.barrier()
+    refs = np.memmap(refs_path, dtype=np.uint8, mode="r", shape=(n_ref, 150))
+    t0 = time.time()
+    reads, truth = synth.simulate_reads_range(g, D.rank * Q, (D.rank + 1) * Q, seed=9)
+    queries = synth.tag(reads)
+    q_emb = synth.embed(queries)
+    log(f"[bench] {Q} reads simulated + embedded in {time.time() - t0:.1f}s")
+    return {"Q": Q, "refs": refs, "index_path": index_path, "q_emb": q_emb, "queries": queries, "truth": truth,
+            "desc": f"C5 per-GPU slice: synthetic 50M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200, "
+                    f"GPU-built), replicated per GPU, {Q} reads per GPU, search + SW rerank, EF=128 K=128"}
 
 
 def gather_results(D, dev, n_total, bufs, local_host):
@@ -195,7 +256,7 @@ def run_c4(args, D):
     ndev = device_count()
     set_device(D.local_rank % max(ndev, 1))
     N = D.world
-    Q = args.queries if args.queries != 100_000 else 1_000_000
+    Q = args.queries or 1_000_000
     w = synth.Workload("c4", 20_000_299, N * Q, stride=4, seed=43, read_seed=8)
     if D.rank == 0:
         t0 = time.time()
@@ -279,7 +340,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--queries", type=int, default=100_000, help="reads per GPU (weak scaling)")
+    ap.add_argument("--queries", type=int, default=0, help="reads per GPU (weak scaling); 0 = the workload's own")
     ap.add_argument("--ef", type=int, default=128)
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--cache", default=os.environ.get("DRM_BENCH_CACHE", "/tmp/drm_bench_cache"))
@@ -287,10 +348,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--build-threads", type=int, default=0)
     ap.add_argument("--index", choices=["pq", "flat"], default="pq",
-                    help="flat (default): hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib "
-                         "defaults), configs[1]'s L2 HNSW search; pq: faiss IndexHNSWPQ, the live pipeline's index")
-    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
-                    help="c3 (default, the headline): search + SW rerank; c4: search only on a 10M-vector "
+                    help="pq (default): faiss IndexHNSWPQ, the live pipeline's index (src/main.cpp:236-237); flat: "
+                         "hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib defaults) over the C3 windows")
+    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c5",
+                    help="c5 (default): the metric's configuration (50M windows, 1.25M reads per GPU), search + SW "
+                         "rerank; c3: 1M windows, 100k reads per GPU, search + SW rerank; c4: search only on a 10M-vector "
                          "sparse (stride 4) index, SURVEY.md sec. 8d")
     args = ap.parse_args()
     _claim_stdout()
@@ -308,28 +370,23 @@ def main():
     ndev = device_count()
     dev = D.local_rank % max(ndev, 1)  # one rank per GPU; ranks share GPUs only on smaller boxes
     set_device(dev)
-    N, Q, K, EF = D.world, args.queries, args.k, args.ef
-    w = synth.Workload("c3", 500_149, N * Q, seed=42, read_seed=7)
-    # rank 0 builds the shared index file; the others wait, then every rank loads its own replica
-    if D.rank == 0:
-        t0 = time.time()
-        w.generate(args.cache, nthreads=args.build_threads, log=log)
-        log(f"[bench] workload ready in {time.time() - t0:.1f}s: {len(w.refs)} windows, index {w.index_path}")
-    D.barrier()
-    if D.rank != 0:
-        w.generate(args.cache)
-    lo, hi = shard_range(N * Q, D.rank, N)  # contiguous query shard of this rank
-    q_emb = np.ascontiguousarray(w.q_emb[lo:hi])
-    queries = np.ascontiguousarray(w.queries[lo:hi])
-    truth = w.truth[lo:hi]
-
+    N, K, EF = D.world, args.k, args.ef
     flat = args.index == "flat"
+    if args.workload == "c5":
+        if flat:
+            raise SystemExit("--index flat is a C3 variant")
+        wl = prepare_c5(args, D, dev)
+    else:
+        wl = prepare_c3(args, D, dev)
+    Q = wl["Q"]
+    q_emb, queries, truth, refs = wl["q_emb"], wl["queries"], wl["truth"], wl["refs"]
+
     if flat:
         from deepreadmapper_amd.flat import HnswFlatIndex
         fpath = os.path.join(args.cache, "c3_flat_M64_efc128.hnsw")
         if D.rank == 0 and not os.path.exists(fpath):
             t0 = time.time()
-            synth.build_flat_index(synth.embed(synth.tag(w.refs)), fpath + ".tmp", M=64, efc=128,
+            synth.build_flat_index(synth.embed(synth.tag(refs)), fpath + ".tmp", M=64, efc=128,
                                    nthreads=args.build_threads)
             os.replace(fpath + ".tmp", fpath)
             log(f"[bench] hnswlib fp32 index built in {time.time() - t0:.1f}s")
@@ -337,8 +394,12 @@ def main():
         ix = HnswFlatIndex(fpath, dev)
         d_L = DeviceBuffer((Q, K), np.uint64)
     else:
-        ix = HnswPqIndex(w.index_path, dev)
-    table = WindowTable(w.refs, dev)
+        t0 = time.time()
+        ix = HnswPqIndex(wl["index_path"], dev)
+        log(f"[bench] index loaded in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    table = WindowTable(refs, dev)
+    log(f"[bench] window table ({len(refs)} x {refs.shape[1]} B) uploaded in {time.time() - t0:.1f}s")
     d_x = DeviceBuffer.from_host(q_emb)
     d_q = DeviceBuffer.from_host(queries)
     d_ql = DeviceBuffer.from_host(np.full(Q, queries.shape[1], dtype=np.int32))
@@ -408,7 +469,7 @@ def main():
         codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
         bytes_launch = float(bytes_q.sum() + codebook)
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
-    cells = float(Q) * K * w.refs.shape[1] * queries.shape[1]
+    cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
     prof_path, pmc = committed_pmc(search_kernel)
     traffic = None
@@ -428,10 +489,9 @@ def main():
     if D.rank == 0:
         cpu = None
         if N == 1 and not args.no_cpu:
-            cpu = cpu_baseline(w, fpath if flat else w.index_path, queries, q_emb, K, EF, args.cpu_budget, log,
+            cpu = cpu_baseline(refs, fpath if flat else wl["index_path"], queries, q_emb, K, EF, args.cpu_budget, log,
                                flat=flat)
-        workload = ("C3: synthetic 1M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200), search + SW "
-                    "rerank, EF=128 K=128") if not flat else (
+        workload = wl["desc"] if not flat else (
                     "C3-flat: the same 1M windows in an hnswlib fp32-L2 index (M=64, EFC=128), hnswlib searchKnn + "
                     "SW rerank, EF=128 K=128")
         result = {
@@ -443,7 +503,7 @@ def main():
                 " + int32 (SW DP, bit-profile u16 kernel)" if os.environ.get("DRM_SW_BITPROFILE") == "1" else
                 " + fp16 fixed-point SW DP (2^-10 units, exact for scores < 1024)"),
             "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
-            "config": {"workload": workload, "n_refs": int(len(w.refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
+            "config": {"workload": workload, "n_refs": int(len(refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
             "roofline": {"bound": "hbm", "kernel": search_kernel, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

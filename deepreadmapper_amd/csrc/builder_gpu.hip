@@ -570,6 +570,11 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
             DRM_HIP_CHECK(hipGetLastError());
         }
         start += cnt;
+        if (verbose && (cnt >= kMaxBatch || start >= n)) {
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            std::fprintf(stderr, "[gpu build] %lld / %lld inserted %.1fs\n", (long long)start, (long long)n,
+                         secs_since(t0));
+        }
     }
     DRM_HIP_CHECK(hipDeviceSynchronize());
     if (verbose)

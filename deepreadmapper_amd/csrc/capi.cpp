@@ -6,6 +6,7 @@
 #include <cstring>
 #include <memory>
 #include <numeric>
+#include <thread>
 #include <unordered_set>
 
 #include "drm_device.h"
@@ -201,27 +202,39 @@ int drm_index_load(const char *path, int device, drm_index **out)
         std::vector<int32_t> nbr0((size_t)n * d.deg0);
         std::vector<uint32_t> upper_off((size_t)n, ~0u);
         std::vector<int32_t> upper;
+        // level-0 rows and the duplicate-link check in parallel (tens of millions of rows at C5)
+        {
+            const int nt = (int)std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+            std::vector<int> dup(nt, 0);
+            std::vector<std::thread> pool;
+            for (int t = 0; t < nt; ++t)
+                pool.emplace_back([&, t] {
+                    for (int64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+                        const uint64_t o = h.offsets[(size_t)i];
+                        int32_t *r = &nbr0[(size_t)i * d.deg0];
+                        std::memcpy(r, &h.neighbors[o + h.cum_nneighbor_per_level[0]], sizeof(int32_t) * d.deg0);
+                        // a row listing one id twice changes visited-set semantics: flag it for the kernel
+                        for (int a = 0; a < d.deg0 && r[a] >= 0 && !dup[t]; ++a)
+                            for (int b = a + 1; b < d.deg0 && r[b] >= 0; ++b)
+                                if (r[a] == r[b]) {
+                                    dup[t] = 1;
+                                    break;
+                                }
+                    }
+                });
+            for (auto &th : pool)
+                th.join();
+            d.has_dup_links = *std::max_element(dup.begin(), dup.end());
+        }
         for (int64_t i = 0; i < n; ++i) {
-            const uint64_t o = h.offsets[(size_t)i];
-            std::memcpy(&nbr0[(size_t)i * d.deg0], &h.neighbors[o + h.cum_nneighbor_per_level[0]],
-                        sizeof(int32_t) * d.deg0);
             const int lv = h.levels[(size_t)i];
             if (lv > 1) {
+                const uint64_t o = h.offsets[(size_t)i];
                 if (upper.size() > 0xF0000000ull)
                     throw Error(DRM_ERR_UNSUPPORTED, "upper-level link table exceeds 32-bit offsets");
                 upper_off[(size_t)i] = (uint32_t)upper.size();
                 upper.insert(upper.end(), h.neighbors.begin() + (o + h.cum_nneighbor_per_level[1]),
                              h.neighbors.begin() + (o + h.cum_nneighbor_per_level[lv]));
-            }
-            // a row listing one id twice changes visited-set semantics: flag it for the kernel
-            if (!d.has_dup_links) {
-                const int32_t *r = &nbr0[(size_t)i * d.deg0];
-                for (int a = 0; a < d.deg0 && r[a] >= 0 && !d.has_dup_links; ++a)
-                    for (int b = a + 1; b < d.deg0 && r[b] >= 0; ++b)
-                        if (r[a] == r[b]) {
-                            d.has_dup_links = 1;
-                            break;
-                        }
             }
         }
         d.upper_len = (int64_t)upper.size();
@@ -666,9 +679,20 @@ int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int6
         const size_t bytes = (size_t)std::max<int64_t>(n_ref, 1) * (size_t)r->dev.row_stride;
         DRM_HIP_CHECK(hipMalloc(&r->dev.windows, bytes));
         DRM_HIP_CHECK(hipMemset(r->dev.windows, 0, bytes));
-        if (n_ref > 0) {
-            DRM_HIP_CHECK(hipMemcpy2D(r->dev.windows, (size_t)r->dev.row_stride, windows, (size_t)row_stride,
-                                      (size_t)ref_len, (size_t)n_ref, hipMemcpyHostToDevice));
+        if (n_ref > 0 && ref_len > 0) {
+            // pageable host rows of ref_len bytes: a 2D host-to-device copy of tens of millions of short
+            // rows is slow, so contiguous chunks go up in 1D copies and are re-pitched on the device
+            const int64_t chunk = std::max<int64_t>(1, ((int64_t)256 << 20) / row_stride);
+            uint8_t *stage = nullptr;
+            DRM_HIP_CHECK(hipMalloc(&stage, (size_t)std::min(chunk, n_ref) * (size_t)row_stride));
+            for (int64_t r0 = 0; r0 < n_ref; r0 += chunk) {
+                const int64_t nr = std::min(chunk, n_ref - r0);
+                DRM_HIP_CHECK(hipMemcpy(stage, windows + r0 * row_stride, (size_t)nr * (size_t)row_stride,
+                                        hipMemcpyHostToDevice));
+                DRM_HIP_CHECK(hipMemcpy2D(r->dev.windows + r0 * r->dev.row_stride, (size_t)r->dev.row_stride, stage,
+                                          (size_t)row_stride, (size_t)ref_len, (size_t)nr, hipMemcpyDeviceToDevice));
+            }
+            DRM_HIP_CHECK(hipFree(stage));
         }
         *out = r.release();
     });

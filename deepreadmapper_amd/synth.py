@@ -65,6 +65,43 @@ def simulate_reads(g, n, read_len=150, sub_rate=0.01, seed=7):
     return reads, names, (2 * pos + strand).astype(np.int64)
 
 
+READ_BLOCK = 1 << 16
+
+
+def simulate_reads_range(g, lo, hi, read_len=150, sub_rate=0.01, seed=7, block=READ_BLOCK):
+    """Reads [lo, hi) of an unbounded seeded read stream, generated in fixed blocks of `block` reads
+    (block b from default_rng([seed, b])), so any shard of a C5-sized batch (10M reads) is produced
+    without materialising the others: rank r of N gets the same reads whatever N is. Same model as
+    simulate_reads (uniform position and strand, `sub_rate` substitutions); names are omitted."""
+    g = np.asarray(g, dtype=np.uint8)
+    n = max(0, hi - lo)
+    reads = np.empty((n, read_len), dtype=np.uint8)
+    truth = np.empty(n, dtype=np.int64)
+    L = len(g)
+    for b in range(lo // block, (hi + block - 1) // block if n else lo // block):
+        rng = np.random.default_rng([seed, b])
+        pos = rng.integers(0, L - read_len + 1, size=block)
+        strand = rng.integers(0, 2, size=block)
+        subs = rng.random((block, read_len)) < sub_rate
+        shift = rng.integers(1, 4, size=(block, read_len), dtype=np.uint8)
+        s0, s1 = max(lo, b * block), min(hi, (b + 1) * block)   # the part of block b inside [lo, hi)
+        j = slice(s0 - b * block, s1 - b * block)
+        p, st, sb, sh = pos[j], strand[j], subs[j], shift[j]
+        r = np.lib.stride_tricks.sliding_window_view(g, read_len)[p]
+        rc = st == 1
+        r[rc] = _COMP[r[rc][:, ::-1]]
+        code = _CODE[r]
+        code = np.where(sb, (code + sh) % 4, code)
+        reads[s0 - lo:s1 - lo] = ACGT[code]
+        truth[s0 - lo:s1 - lo] = 2 * p + st
+    return reads, truth
+
+
+_CODE = np.zeros(256, dtype=np.uint8)
+for _i, _c in enumerate(b"ACGT"):
+    _CODE[_c] = _i
+
+
 def tag(reads):
     """format_fastq's "<" + seq + ">" (src/utils/parse_inputs.cpp:905-912) on a [n, L] uint8 array."""
     n, L = reads.shape

@@ -13,10 +13,17 @@ from deepreadmapper_amd.device import DeviceBuffer, synchronize  # noqa: E402
 from deepreadmapper_amd.search import HnswPqIndex  # noqa: E402
 from deepreadmapper_amd._native import lib, check  # noqa: E402
 
-w = synth.Workload("c3", 500_149, 100_000, seed=42, read_seed=7).generate("/tmp/drm_bench_cache")
-ix = HnswPqIndex(w.index_path)
-Q = 100_000
-dq = DeviceBuffer.from_host(w.q_emb[:Q])
+if len(sys.argv) > 1 and sys.argv[1] == "c5":  # bench.py --workload c5 must have run (its cache files)
+    g = synth.genome(25_000_149, seed=44)
+    reads, _ = synth.simulate_reads_range(g, 0, 1_250_000, seed=9)
+    q_emb = synth.embed(synth.tag(reads))
+    index_path = "/tmp/drm_bench_cache/c5_M16_efc200_s1_gpu.index"
+else:
+    w = synth.Workload("c3", 500_149, 100_000, seed=42, read_seed=7).generate("/tmp/drm_bench_cache")
+    q_emb, index_path = w.q_emb, w.index_path
+ix = HnswPqIndex(index_path)
+Q = len(q_emb)
+dq = DeviceBuffer.from_host(q_emb[:Q])
 dD, dI = DeviceBuffer((Q, 128), np.float32), DeviceBuffer((Q, 128), np.int64)
 ix.search_device(dq, Q, 128, 128, dD, dI)
 synchronize()
