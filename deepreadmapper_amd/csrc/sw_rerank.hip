@@ -313,11 +313,16 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
 // v_pk_maximum3_f16 -- 3.5 VALU per cell pair.
 //
 // The match terms come ready-paired from LDS: for candidate-byte codes a, b in 0..4 (A, C, G, T,
-// 4 = "a byte the query does not contain") `pprof` row (a, b) holds the words
+// 4 = "a byte the query does not contain") `pprof` row (a, b) (at a * GST + b * PST words, a layout
+// whose 16 A/C/G/T rows fall on distinct bank quads of every ds_read_b128 lane group) holds the words
 // (q[j]==a ? 0x1800 : 0) | (q[j]==b ? 0x18000000 : 0) (0x1800 = 2^-9 in fp16). A candidate byte that
 // is not A/C/G/T but does occur in the query (e.g. N against N) cannot be coded; the query is then
 // flagged (ncand = kNeedBitProfile) and the bit-profile kernel re-scores it exactly.
 constexpr int kNeedBitProfile = -4;
+#ifndef DRM_SW_BLOCKLOAD
+#define DRM_SW_BLOCKLOAD 1 // candidate bytes by 16-byte block loads (0: one byte load per DP row)
+#endif
+
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
@@ -362,8 +367,14 @@ __device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pp, h2 &
 template <int LQ>
 __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
 {
-    constexpr int PST = ((LQ + 3) & ~3) + 4; // pair-profile row stride in words (+4: bank spread)
-    __shared__ __align__(16) uint32_t pprof[25 * PST];
+    // Pair-profile layout: row (ka, kb) at ka * GST + kb * PST words. A ds_read_b128 lane group (16
+    // lanes) is conflict-free when the 16-byte chunk index (address / 16) mod 16 differs between
+    // distinct rows; with PST / 4 = 7 or 1 (mod 16) and GST / 4 = 4 (mod 16) the 16 A/C/G/T pairs
+    // (ka, kb < 4) land on 16 distinct chunk indices (MI355X_MICROARCH.md, LDS banking).
+    constexpr int PST = ((LQ + 3) & ~3) + 4 + (((((LQ + 3) & ~3) + 4) / 4) % 2 == 0 ? 4 : 0);
+    constexpr int GST = 5 * PST + 4 * (((4 - 5 * (PST / 4)) % 16 + 16) % 16);
+    static_assert((PST / 4) % 2 == 1 && (GST / 4) % 16 == 4, "pair-profile bank spread");
+    __shared__ __align__(16) uint32_t pprof[5 * GST];
     __shared__ __align__(16) uint8_t qbuf[(LQ + 15) & ~15];
     __shared__ uint32_t qmask[8]; // bytes present in the query
     __shared__ uint32_t cand[kMaxCands];
@@ -430,12 +441,12 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         __syncthreads();
         for (int t = tid; t < qlen && t < LQ; t += 64)
             atomicOr(&qmask[qbuf[t] >> 5], 1u << (qbuf[t] & 31));
-        for (int e = tid; e < 25 * PST; e += 64) {
-            const int combo = e / PST, j = e % PST;
+        for (int e = tid; e < 5 * GST; e += 64) {
+            const int ka = e / GST, kb = (e % GST) / PST, j = (e % GST) % PST;
             uint32_t word = 0;
-            if (j < qlen && j < LQ) {
+            if (kb < 5 && j < qlen && j < LQ) {
                 const int c = qbuf[j];
-                word = (c == acgt_byte(combo / 5) ? 0x1800u : 0u) | (c == acgt_byte(combo % 5) ? 0x18000000u : 0u);
+                word = (c == acgt_byte(ka) ? 0x1800u : 0u) | (c == acgt_byte(kb) ? 0x18000000u : 0u);
             }
             pprof[e] = word;
         }
@@ -452,6 +463,39 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 H[j] = (h2){(_Float16)0.0f, (_Float16)0.0f};
             h2 best = {(_Float16)0.0f, (_Float16)0.0f};
             const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
+            // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
+            // block in flight while the current one is consumed), not one byte load per row
+#if DRM_SW_BLOCKLOAD
+            const uint4 *pa = reinterpret_cast<const uint4 *>(a.refs + (size_t)wa * (size_t)a.row_stride);
+            const uint4 *pb = reinterpret_cast<const uint4 *>(a.refs + (size_t)wb * (size_t)a.row_stride);
+            const int L = a.ref_len;
+            const int nblk = (int)(a.row_stride >> 4); // row_stride is a multiple of 16, >= ref_len
+            uint4 ba = make_uint4(0u, 0u, 0u, 0u), bb = ba, na4 = ba, nb4 = ba;
+            if (L > 0) {
+                na4 = pa[0];
+                nb4 = pb[0];
+            }
+            uint32_t wa4 = 0u, wb4 = 0u;
+            for (int i = 0; i < L; ++i) {
+                if ((i & 15) == 0) { // wave-uniform: next block becomes current, prefetch the one after
+                    ba = na4;
+                    bb = nb4;
+                    const int nx = (i >> 4) + 1;
+                    if (nx < nblk && 16 * nx < L) {
+                        na4 = pa[nx];
+                        nb4 = pb[nx];
+                    }
+                }
+                if ((i & 3) == 0) {
+                    const int wsel = (i >> 2) & 3;
+                    wa4 = wsel == 0 ? ba.x : wsel == 1 ? ba.y : wsel == 2 ? ba.z : ba.w;
+                    wb4 = wsel == 0 ? bb.x : wsel == 1 ? bb.y : wsel == 2 ? bb.z : bb.w;
+                } else {
+                    wa4 >>= 8;
+                    wb4 >>= 8;
+                }
+                const int ca = (int)(wa4 & 255u), cb = (int)(wb4 & 255u);
+#else
             const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
             const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
             const int L = a.ref_len;
@@ -463,6 +507,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                     na = pa[i + 1];
                     nb2 = pb[i + 1];
                 }
+#endif
                 int ka = acgt_code(ca), kb = acgt_code(cb);
                 if (ka < 0) {
                     flagged |= ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
@@ -472,7 +517,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                     flagged |= has_b && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
                     kb = 4;
                 }
-                sw_row_f16<LQ>(H, pprof + (ka * 5 + kb) * PST, best);
+                sw_row_f16<LQ>(H, pprof + ka * GST + kb * PST, best);
             }
             a.cand_ids[q * a.cmax + c0] = wa;
             a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);

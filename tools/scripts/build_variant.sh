@@ -7,8 +7,9 @@ NAME=$1; shift
 ROCM=${ROCM:-/opt/rocm}
 mkdir -p ab/$NAME.obj
 FL="-O3 -std=c++17 -fPIC -Iinclude -Ideepreadmapper_amd/csrc -Wall -Wno-unused-result --offload-arch=gfx950 -ffp-contract=off -munsafe-fp-atomics $*"
-for k in hnsw_search hnsw_search_lds hnsw_flat_search sw_rerank query_order; do
-  $ROCM/bin/hipcc $FL -c deepreadmapper_amd/csrc/$k.hip -o ab/$NAME.obj/$k.o &
+for f in deepreadmapper_amd/csrc/*.hip; do
+  k=$(basename $f .hip)
+  $ROCM/bin/hipcc $FL -c $f -o ab/$NAME.obj/$k.o &
 done
 wait
 $ROCM/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$NAME.so ab/$NAME.obj/*.o build/capi.o build/faiss_io.o \
