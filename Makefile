@@ -16,7 +16,7 @@ HOSTFLAGS := $(COMMON) -fopenmp -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I$(ROC
 
 LIB := $(PKG)/libdrm_hip.so
 HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/hnsw_pq_fast.o $(BUILD)/builder_gpu.o $(BUILD)/embed_gpu.o $(BUILD)/hnsw_search_lds.o $(BUILD)/hnsw_flat_search.o $(BUILD)/sw_rerank.o \
-            $(BUILD)/capi.o
+            $(BUILD)/capi.o $(BUILD)/exec.o
 HOST_OBJS := $(BUILD)/faiss_io.o $(BUILD)/formats.o $(BUILD)/builder.o $(BUILD)/embed.o $(BUILD)/hnswlib_io.o \
              $(BUILD)/builder_flat.o
 HDRS := include/drm_hip.h $(SRC)/drm_internal.h $(SRC)/drm_device.h $(SRC)/pq_common.h
@@ -32,11 +32,14 @@ $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 $(BUILD)/capi.o: $(SRC)/capi.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
+$(BUILD)/exec.o: $(SRC)/exec.cpp $(HDRS) | $(BUILD)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
 $(BUILD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BUILD)
 	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(HIP_OBJS) $(HOST_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lgomp -Wl,-soname,libdrm_hip.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -Wl,-soname,libdrm_hip.so
 
 bin/%: tools/%.cpp $(LIB) $(HDRS) | $(BUILD)
 	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -ldrm_hip -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(PKG)' -Wl,-rpath,$(ROCM)/lib

@@ -50,11 +50,11 @@ def cpu_model():
     return "unknown"
 
 
-def committed_pmc(kernel_substr):
-    """Per-dispatch PMC summary of `kernel_substr` from the newest committed profile
-    (profiles/rNN/summary.json, written by tools/scripts/profile.sh + summarize_profile.py)."""
+def committed_pmc(kernel_substr, workload):
+    """Per-dispatch PMC summary of `kernel_substr` on `workload` from the newest committed profile
+    (profiles/rNN/summary_<workload>.json, written by tools/scripts/profile.sh + summarize_profile.py)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"summary_{workload}.json")), reverse=True):
         try:
             ks = json.load(open(path))["kernels"]
         except (OSError, ValueError, KeyError):
@@ -96,7 +96,7 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.dist = None
-        self.nccl = None  # RCCL group for the end-of-run result gather
+        self.comm = None  # RCCL communicator (drm_comm) for the end-of-run result gather
         if self.world > 1:
             import torch.distributed as dist  # imported before libdrm_hip.so is loaded
             dist.init_process_group("gloo")
@@ -115,6 +115,8 @@ class Dist:
         return float(t.item())
 
     def close(self):
+        if self.comm is not None:
+            self.comm.free()
         if self.dist:
             self.dist.destroy_process_group()
 
@@ -216,29 +218,38 @@ def prepare_c5(args, D, dev):
 
 
 def gather_results(D, dev, n_total, bufs, local_host):
-    """End-of-run exchange: every rank's result rows are all-gathered to rank 0 over
-    RCCL (torch.distributed nccl backend, xGMI), outside the timed region, and rank 0 checks its own
-    shard in the gathered arrays. Reported, never fatal: the scaling numbers stand either way."""
+    """End-of-run exchange: every rank's device-resident result rows are gathered to
+    rank 0 over RCCL by the library's own C++ path (drm_comm_gather_rows: grouped ncclSend/ncclRecv over
+    xGMI), outside the timed region; the RCCL unique id travels over the gloo control plane. Rank 0
+    checks its own shard in the gathered rows. Reported, never fatal: the scaling numbers stand either
+    way."""
     if D.world == 1:
         return None
     try:
-        import torch
-        from deepreadmapper_amd.shard import gather_rows_device
-        torch.cuda.set_device(dev)
-        if D.nccl is None:
-            D.nccl = D.dist.new_group(backend="nccl")
-        torch.cuda.synchronize()
+        from deepreadmapper_amd.device import DeviceBuffer, synchronize
+        from deepreadmapper_amd.executor import Comm
+        from deepreadmapper_amd.shard import shard_range
+        if D.comm is None:
+            obj = [Comm.unique_id() if D.rank == 0 else None]
+            D.dist.broadcast_object_list(obj, src=0)
+            D.comm = Comm(obj[0], D.world, D.rank, dev)
+        synchronize()
         t0 = time.perf_counter()
-        full = {name: gather_rows_device(b, n_total, D.rank, D.world, D.dist, group=D.nccl) for name, b in bufs}
-        torch.cuda.synchronize()
+        full, nbytes = {}, 0
+        for name, b in bufs:
+            row = b.nbytes // b.shape[0]
+            recv = DeviceBuffer((n_total,) + tuple(b.shape[1:]), b.dtype) if D.rank == 0 else None
+            D.comm.gather_rows(b, n_total, row, recv, root=0)
+            full[name] = recv
+            nbytes += b.nbytes
+        synchronize()
         ms = (time.perf_counter() - t0) * 1e3
-        out = {"backend": "nccl (RCCL)", "ms": round(ms, 3),
-               "bytes_per_rank": int(sum(b.nbytes for _, b in bufs))}
+        out = {"backend": "RCCL (drm_comm_gather_rows, C++)", "ms": round(ms, 3), "bytes_per_rank": int(nbytes)}
         if D.rank == 0:
-            from deepreadmapper_amd.shard import shard_range
             lo, hi = shard_range(n_total, 0, D.world)
-            out["rank0_shard_matches"] = bool(all(np.array_equal(full[k][lo:hi], v) for k, v in local_host.items()))
-            out["rows"] = int(full[bufs[0][0]].shape[0])
+            out["rank0_shard_matches"] = bool(all(np.array_equal(full[k].download()[lo:hi], v)
+                                                  for k, v in local_host.items()))
+            out["rows"] = int(n_total)
         return out
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         return {"error": f"{type(e).__name__}: {e}"}
@@ -471,11 +482,11 @@ def main():
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
     cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
-    prof_path, pmc = committed_pmc(search_kernel)
+    prof_path, pmc = committed_pmc(search_kernel, args.workload + ("_flat" if flat else ""))
     traffic = None
     if pmc and "hbm_bytes_est" in pmc:
         traffic = float(pmc["hbm_bytes_est"])
-    sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL)
+    sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, args.workload)
     ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
     sw_gcups = cells / (sw_ms * 1e-3) / 1e9
     # VALU issue ceiling of the SW DP: 4 SIMD x 16 lanes per CU, 2 cells per packed lane-op

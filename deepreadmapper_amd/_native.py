@@ -31,6 +31,9 @@ EXPORTS = [
     "drm_embed_kmer3_device",
     "drm_flat_index_load", "drm_flat_index_free", "drm_flat_index_get_info", "drm_flat_search",
     "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_fallbacks",
+    "drm_refs_get_info", "drm_host_alloc", "drm_host_free", "drm_search_rerank", "drm_multi_create",
+    "drm_multi_free", "drm_multi_get_index_info", "drm_multi_search_rerank", "drm_comm_unique_id", "drm_comm_init",
+    "drm_comm_free", "drm_comm_gather_rows",
 ]
 
 
@@ -46,7 +49,7 @@ class IndexInfo(C.Structure):
     _fields_ = [("d", C.c_int32), ("ntotal", C.c_int64), ("pq_M", C.c_int32), ("pq_nbits", C.c_int32),
                 ("M_hnsw", C.c_int32), ("max_level", C.c_int32), ("entry_point", C.c_int32),
                 ("efConstruction", C.c_int32), ("efSearch", C.c_int32), ("metric_type", C.c_int32),
-                ("device_bytes", C.c_int64)]
+                ("device_bytes", C.c_int64), ("device", C.c_int32)]
 
 
 class FlatIndexInfo(C.Structure):
@@ -118,6 +121,20 @@ def lib():
         "drm_build_hnswpq_device": (C.c_int, [vp, i64, i32, i32, i32, i32, i32, C.c_double, C.c_uint64, C.c_int,
                                               C.c_char_p]),
         "drm_embed_kmer3_device": (C.c_int, [vp, i64, i32, i64, i32, C.c_uint64, vp, vp]),
+        "drm_refs_get_info": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i32), C.POINTER(C.c_int)]),
+        "drm_host_alloc": (C.c_int, [C.POINTER(vp), sz]),
+        "drm_host_free": (C.c_int, [vp]),
+        "drm_search_rerank": (C.c_int, [vp, vp, vp, i64, i32, i32, i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
+                                        C.POINTER(SearchStats)]),
+        "drm_multi_create": (C.c_int, [C.c_char_p, vp, C.c_int, vp, i64, i32, i64, C.POINTER(vp)]),
+        "drm_multi_free": (C.c_int, [vp]),
+        "drm_multi_get_index_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
+        "drm_multi_search_rerank": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, i32, i64, i32, vp, vp, vp, vp,
+                                              vp, C.POINTER(SearchStats)]),
+        "drm_comm_unique_id": (C.c_int, [vp]),
+        "drm_comm_init": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "drm_comm_free": (C.c_int, [vp]),
+        "drm_comm_gather_rows": (C.c_int, [vp, vp, i64, i64, vp, C.c_int, vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -334,6 +334,7 @@ int drm_index_get_info(const drm_index *index, drm_index_info *info)
         info->efSearch = d.meta.efSearch;
         info->metric_type = d.meta.hdr.metric_type;
         info->device_bytes = d.device_bytes;
+        info->device = d.device;
     });
 }
 
@@ -695,6 +696,20 @@ int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int6
             DRM_HIP_CHECK(hipFree(stage));
         }
         *out = r.release();
+    });
+}
+
+int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device)
+{
+    return guarded([&] {
+        if (!refs)
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (n_ref)
+            *n_ref = refs->dev.n_ref;
+        if (ref_len)
+            *ref_len = refs->dev.ref_len;
+        if (device)
+            *device = refs->dev.device;
     });
 }
 

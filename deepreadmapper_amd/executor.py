@@ -1,0 +1,133 @@
+"""Batch executor (csrc/exec.cpp): the fused search -> SW rerank pass of the reference's batch driver
+(faiss_search then post_process_sw_static, src/main.cpp:278, :333-341), its multi-GPU fan-out
+(replicated index, contiguous query shards) and the RCCL gather of device-resident
+result rows across the ranks of a one-process-per-GPU job."""
+import ctypes as C
+
+import numpy as np
+
+from ._native import IndexInfo, SearchStats, check, lib, ptr
+
+
+def _outputs(n, k_clusters, k, rerank):
+    out = {"D": np.empty((n, k_clusters), dtype=np.float32), "I": np.empty((n, k_clusters), dtype=np.int64)}
+    if rerank:
+        out.update(sw_scores=np.empty((n, k), dtype=np.int32), sw_ids=np.empty((n, k), dtype=np.uint64),
+                   status=np.empty(n, dtype=np.int32))
+    return out
+
+
+def _query_args(x, queries):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    if x.ndim != 2:
+        raise ValueError("embeddings must be [n, d]")
+    if queries is None:
+        return x, None, None, 0
+    if isinstance(queries, tuple):  # (qbuf [n, q_stride] u8, q_len [n] i32), e.g. rerank.pack_queries
+        qbuf, ql = queries
+    else:
+        qbuf = np.ascontiguousarray(queries, dtype=np.uint8)
+        ql = np.full(len(qbuf), qbuf.shape[1], dtype=np.int32)
+    qbuf, ql = np.ascontiguousarray(qbuf, dtype=np.uint8), np.ascontiguousarray(ql, dtype=np.int32)
+    if len(qbuf) != len(x) or len(ql) != len(x):
+        raise ValueError("one query sequence per embedding")
+    return x, qbuf, ql, qbuf.shape[1]
+
+
+def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None, stride=1):
+    """drm_search_rerank: search (k_clusters results) then, when `table` (WindowTable) and `queries`
+    are given, the SW rerank to k. Returns a dict of D, I (+ sw_scores, sw_ids, status) and stats."""
+    kc = k if k_clusters is None else k_clusters
+    x, qbuf, ql, qs = _query_args(x, queries)
+    rr = table is not None and qbuf is not None
+    o = _outputs(len(x), kc, k, rr)
+    st = SearchStats()
+    check(lib().drm_search_rerank(index.handle, table.handle if rr else None, ptr(x), len(x), x.shape[1], int(kc),
+                                  int(ef), ptr(qbuf) if rr else None, ptr(ql) if rr else None, qs, int(stride),
+                                  int(k), ptr(o["D"]), ptr(o["I"]), ptr(o.get("sw_scores")), ptr(o.get("sw_ids")),
+                                  ptr(o.get("status")), C.byref(st)))
+    o["stats"] = st
+    return o
+
+
+class MultiIndex:
+    """drm_multi: one IndexHNSWPQ replica (+ window table) per entry of `devices` (repeats allowed)."""
+
+    def __init__(self, path, devices, windows=None):
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = C.c_void_p()
+        if windows is not None:
+            w = np.ascontiguousarray(windows, dtype=np.uint8)
+            check(lib().drm_multi_create(str(path).encode(), ptr(devs), len(devs), ptr(w), w.shape[0], w.shape[1],
+                                         w.shape[1], C.byref(h)))
+        else:
+            check(lib().drm_multi_create(str(path).encode(), ptr(devs), len(devs), None, 0, 0, 0, C.byref(h)))
+        self._h = h.value
+        self.devices = list(devs)
+        self.has_refs = windows is not None
+        info = IndexInfo()
+        check(lib().drm_multi_get_index_info(self._h, C.byref(info)))
+        self.info = info
+
+    def search_rerank(self, x, queries=None, k=128, ef=128, k_clusters=None, stride=1):
+        kc = k if k_clusters is None else k_clusters
+        x, qbuf, ql, qs = _query_args(x, queries)
+        rr = self.has_refs and qbuf is not None
+        o = _outputs(len(x), kc, k, rr)
+        st = SearchStats()
+        check(lib().drm_multi_search_rerank(self._h, ptr(x), len(x), x.shape[1], int(kc), int(ef),
+                                            ptr(qbuf) if rr else None, ptr(ql) if rr else None, qs, int(stride),
+                                            int(k), ptr(o["D"]), ptr(o["I"]), ptr(o.get("sw_scores")),
+                                            ptr(o.get("sw_ids")), ptr(o.get("status")), C.byref(st)))
+        o["stats"] = st
+        return o
+
+    def free(self):
+        if self._h:
+            check(lib().drm_multi_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+class Comm:
+    """drm_comm: RCCL communicator of a one-process-per-GPU job. Rank 0 makes the id (unique_id()); the
+    job hands it to every rank out of band (bench.py: torch.distributed gloo broadcast)."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * Comm.ID_BYTES)()
+        check(lib().drm_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid, nranks, rank, device):
+        if len(uid) != Comm.ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        buf = (C.c_uint8 * Comm.ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().drm_comm_init(buf, int(nranks), int(rank), int(device), C.byref(h)))
+        self._h = h.value
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+
+    def gather_rows(self, d_send, n_total, row_bytes, d_recv=None, root=0, stream=None):
+        """Rows [r*n/G, (r+1)*n/G) of every rank's d_send (DeviceBuffer) land in the root's d_recv."""
+        check(lib().drm_comm_gather_rows(self._h, d_send.ptr, int(n_total), int(row_bytes),
+                                         d_recv.ptr if d_recv is not None else None, int(root),
+                                         stream.handle if stream is not None else None))
+
+    def free(self):
+        if self._h:
+            check(lib().drm_comm_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001
+            pass

@@ -45,6 +45,7 @@ typedef struct {
     int32_t efSearch;      /* value stored in the file                          */
     int32_t metric_type;   /* 1 = METRIC_L2 (the only one the reference builds) */
     int64_t device_bytes;  /* HBM held by the index on its device              */
+    int32_t device;        /* HIP device the index lives on                     */
 } drm_index_info;
 
 typedef struct {
@@ -155,6 +156,8 @@ int drm_sw_scores(const uint8_t *s1, const int64_t *off1, const int32_t *len1, c
 int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int64_t row_stride, int device,
                     drm_refs **out);
 int drm_refs_free(drm_refs *refs);
+/* Shape and device of a window table (any out-pointer may be NULL). */
+int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device);
 
 /* post_process_sw_static (src/utils/post_processor.cpp:454-549) -> find_sequences (static,
  * :204-336) -> sw_reranker (src/utils/reranker.cpp:3-51) -> calc_sw_score, for nq queries.
@@ -177,6 +180,62 @@ int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors
                                       const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
                                       int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
                                       uint64_t *d_top_ids, int32_t *d_status, void *stream);
+
+/* ---------------------------------------------------------------- batch executor (exec.cpp)
+ * Pinned host memory: buffers from drm_host_alloc make the executor's host <-> device copies DMA
+ * transfers that overlap the kernels; ordinary (pageable) buffers work too, staged by the runtime. */
+int drm_host_alloc(void **ptr, size_t bytes);
+int drm_host_free(void *ptr);
+
+/* The fused search -> SW rerank of one batch driver pass (SURVEY.md sec. 8b `drm_search_rerank`): the
+ * reference's faiss_search(index, emb, k_clusters, ef) followed by post_process_sw_static(neighbors,
+ * distances, ref_seqs, query_seqs, ref_len, stride, k, k_clusters) (src/main.cpp:278, :333-341), run as
+ * batches streamed through the device (host->device copies, kernels and device->host copies of
+ * consecutive batches overlap on three streams; batch size DRM_BATCH, default 262144 queries).
+ * Host pointers throughout:
+ *   x [n x d] f32 -> D [n x k_clusters] f32, I [n x k_clusters] int64 (drm_search's outputs);
+ *   refs == NULL: search only (queries ... status ignored);
+ *   else queries [n x q_stride] bytes with q_len[n] -> sw_scores / sw_ids [n x k] and status[n]
+ *   (drm_post_process_sw_static_device's per-query status: k or 0 rows emitted, -1 not enough
+ *   candidates, -2 / -3 candidate or length limits).
+ * Errors: those of drm_search, plus DRM_ERR_K / DRM_ERR_CANDS / DRM_ERR_UNSUPPORTED as
+ * drm_post_process_sw_static reports them (the outputs of the other queries are still written).
+ * stats->kernel_ms is the device span of the compute stream. */
+int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, int32_t d, int32_t k_clusters,
+                      int32_t ef, const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                      int32_t k, float *D, int64_t *I, int32_t *sw_scores, uint64_t *sw_ids, int32_t *status,
+                      drm_search_stats *stats);
+
+/* ---------------------------------------------------------------- multi-GPU fan-out
+ * One index replica (and window table, when windows != NULL) per entry of devices[ndev] -- the same
+ * device may appear more than once. drm_multi_search_rerank splits the n queries into contiguous
+ * shards [r*n/ndev, (r+1)*n/ndev), runs drm_search_rerank for shard r on devices[r] from its own host
+ * thread, and writes every shard straight into the caller's outputs (same arguments and outputs as
+ * drm_search_rerank; stats summed, kernel_ms the slowest shard). Outputs are byte-identical to a
+ * one-device run: queries are independent (src/utils/post_processor.cpp:491). */
+typedef struct drm_multi drm_multi;
+int drm_multi_create(const char *index_path, const int *devices, int ndev, const uint8_t *windows, int64_t n_ref,
+                     int32_t ref_len, int64_t row_stride, drm_multi **out);
+int drm_multi_free(drm_multi *m);
+int drm_multi_get_index_info(const drm_multi *m, drm_index_info *info); /* replica 0's info */
+int drm_multi_search_rerank(drm_multi *m, const float *x, int64_t n, int32_t d, int32_t k_clusters, int32_t ef,
+                            const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride, int32_t k,
+                            float *D, int64_t *I, int32_t *sw_scores, uint64_t *sw_ids, int32_t *status,
+                            drm_search_stats *stats);
+
+/* ---------------------------------------------------------------- RCCL result gather (one process per GPU)
+ * A communicator over the nranks processes of a job (rank 0 creates the id with drm_comm_unique_id and
+ * hands it to the others out of band, e.g. over the job's gloo/TCP control plane).
+ * drm_comm_gather_rows: rank r holds rows [r*n_total/nranks, (r+1)*n_total/nranks) of a row-major
+ * [n_total x row_bytes] result in d_send (device memory); the root receives all n_total rows in d_recv
+ * over RCCL point-to-point transfers (xGMI), enqueued on `stream`. */
+#define DRM_COMM_ID_BYTES 128
+typedef struct drm_comm drm_comm;
+int drm_comm_unique_id(uint8_t *id);
+int drm_comm_init(const uint8_t *id, int nranks, int rank, int device, drm_comm **out);
+int drm_comm_free(drm_comm *comm);
+int drm_comm_gather_rows(drm_comm *comm, const void *d_send, int64_t n_total, int64_t row_bytes, void *d_recv, int root,
+                         void *stream);
 
 /* ---------------------------------------------------------------- index build (hnswpq_index)
  * build_faiss_index (src/hnswpq/index.cpp:86-193): trains PQ on an evenly spaced sample of

@@ -34,6 +34,20 @@ static void check(int rc)
         throw drm::Error(rc, drm_last_error());
 }
 
+// pinned host buffer (drm_host_alloc): the executor's copies become DMA transfers beside the kernels
+template <class T> struct Pinned {
+    T *p = nullptr;
+    explicit Pinned(size_t n)
+    {
+        void *v = nullptr;
+        check(drm_host_alloc(&v, sizeof(T) * std::max<size_t>(n, 1)));
+        p = static_cast<T *>(v);
+    }
+    ~Pinned() { drm_host_free(p); }
+    Pinned(const Pinned &) = delete;
+    Pinned &operator=(const Pinned &) = delete;
+};
+
 int main(int argc, char *argv[])
 {
     if (argc < 4 || argc > 10) {
@@ -75,9 +89,23 @@ int main(int argc, char *argv[])
         const bool use_streaming = argc >= 10 && std::stoi(argv[9]) != 0;
         if (use_dynamic || use_streaming)
             throw drm::Error(DRM_ERR_UNSUPPORTED, "use_dynamic / use_streaming are not supported by this build");
-        int device = 0;
-        if (const char *dv = std::getenv("DRM_DEVICE"))
-            device = std::atoi(dv);
+        // devices: DRM_DEVICES=0,1,... fans the batch out over several GPUs (contiguous query shards,
+        // replicated index); DRM_DEVICE=i picks one (default 0)
+        std::vector<int> devices;
+        if (const char *dl = std::getenv("DRM_DEVICES")) {
+            std::string sdl(dl);
+            for (size_t p = 0; p < sdl.size();) {
+                size_t q = sdl.find(',', p);
+                if (q == std::string::npos)
+                    q = sdl.size();
+                if (q > p)
+                    devices.push_back(std::stoi(sdl.substr(p, q - p)));
+                p = q + 1;
+            }
+        }
+        if (devices.empty())
+            devices.push_back(std::getenv("DRM_DEVICE") ? std::atoi(std::getenv("DRM_DEVICE")) : 0);
+        const int device = devices[0];
 
         // ---- data loading
         std::vector<float> emb;
@@ -121,21 +149,44 @@ int main(int argc, char *argv[])
         }
         std::cout << "[MAIN] Total Data loading time: " << ms_since(t0) << " ms" << std::endl << std::endl;
 
-        // ---- index
+        // ---- window table (static ref_seqs) as one fixed-width block
+        std::string table;
+        if (!is_npy) {
+            table.assign(refs.size() * ref_len, '\0');
+            for (size_t r = 0; r < refs.size(); ++r)
+                std::memcpy(&table[r * ref_len], refs[r].data(), ref_len);
+        }
+
+        // ---- index (one replica per device)
         t0 = clk::now();
         if (!std::filesystem::exists(index_file))
             throw drm::Error(DRM_ERR_IO, "Index file does not exist: " + index_file);
         drm_index *index = nullptr;
-        check(drm_index_load(index_file.c_str(), device, &index));
+        drm_refs *rt = nullptr;
+        drm_multi *multi = nullptr;
         drm_index_info info;
-        check(drm_index_get_info(index, &info));
+        if (devices.size() == 1) {
+            check(drm_index_load(index_file.c_str(), device, &index));
+            check(drm_index_get_info(index, &info));
+            if (!is_npy)
+                check(drm_refs_create((const uint8_t *)table.data(), (int64_t)refs.size(), (int32_t)ref_len,
+                                      (int64_t)ref_len, device, &rt));
+        } else {
+            check(drm_multi_create(index_file.c_str(), devices.data(), (int)devices.size(),
+                                   is_npy ? nullptr : (const uint8_t *)table.data(), (int64_t)refs.size(),
+                                   (int32_t)ref_len, (int64_t)ref_len, &multi));
+            check(drm_multi_get_index_info(multi, &info));
+        }
         std::cout << "[MAIN] Index loaded time: " << ms_since(t0) << " ms (" << info.ntotal << " vectors, "
-                  << info.device_bytes / (1 << 20) << " MiB on device " << device << ")" << std::endl;
+                  << info.device_bytes / (1 << 20) << " MiB on each of " << devices.size() << " device(s))"
+                  << std::endl;
 
-        // ---- embedding (stand-in for the OpenVINO model)
+        // ---- embedding (stand-in for the OpenVINO model), into pinned host memory
+        if (!is_npy)
+            dim = (size_t)info.d;
+        Pinned<float> x(nq * dim);
         if (!is_npy) {
             t0 = clk::now();
-            dim = (size_t)info.d;
             std::string all;
             std::vector<int64_t> off(nq);
             std::vector<int32_t> len(nq);
@@ -144,53 +195,57 @@ int main(int argc, char *argv[])
                 len[i] = (int32_t)qseqs[i].size();
                 all += qseqs[i];
             }
-            emb.resize(nq * dim);
             check(drm_embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)nq, (int32_t)dim,
-                                  drm::kEmbedSeed, emb.data()));
+                                  drm::kEmbedSeed, x.p));
             std::cout << "[MAIN] Inference (3-mer stand-in) time: " << ms_since(t0) << " ms" << std::endl;
+        } else {
+            std::memcpy(x.p, emb.data(), sizeof(float) * nq * dim);
         }
 
-        // ---- HNSW search (faiss_search(alg_hnsw, embeddings, k_clusters, ef), src/main.cpp:278)
+        // ---- HNSW search (faiss_search(alg_hnsw, embeddings, k_clusters, ef), src/main.cpp:278) streamed into
+        //      the SW rerank (post_process_sw_static, :333-341) batch by batch
+        size_t qs = 0;
+        for (auto &q : qseqs)
+            qs = std::max(qs, q.size());
+        Pinned<uint8_t> qbuf(nq * std::max<size_t>(qs, 1));
+        Pinned<int32_t> ql(nq), status(nq);
+        for (size_t i = 0; i < nq && !is_npy; ++i) {
+            std::memset(qbuf.p + i * qs, 0, qs);
+            std::memcpy(qbuf.p + i * qs, qseqs[i].data(), qseqs[i].size());
+            ql.p[i] = (int32_t)qseqs[i].size();
+        }
+        Pinned<float> D(nq * (size_t)k_clusters);
+        Pinned<int64_t> I(nq * (size_t)k_clusters);
+        Pinned<int32_t> sw_scores(is_npy ? 0 : nq * (size_t)k);
+        Pinned<uint64_t> sw_ids(is_npy ? 0 : nq * (size_t)k);
         t0 = clk::now();
-        std::vector<float> D(nq * (size_t)k_clusters);
-        std::vector<int64_t> I(nq * (size_t)k_clusters);
         drm_search_stats st{};
-        check(drm_search(index, emb.data(), (int64_t)nq, (int32_t)dim, k_clusters, ef, D.data(), I.data(), &st));
-        std::cout << "[MAIN] Search time: " << ms_since(t0) << " ms (kernel " << st.kernel_ms << " ms, ndis "
-                  << st.ndis << ", nhops " << st.nhops << ")" << std::endl;
-        check(drm_index_free(index));
-
-        // ---- SW rerank (post_process_sw_static)
-        std::vector<int32_t> sw_scores;
-        std::vector<uint64_t> sw_ids;
-        if (!is_npy) {
-            t0 = clk::now();
-            drm_refs *rt = nullptr;
-            std::string table(refs.size() * ref_len, '\0');
-            for (size_t r = 0; r < refs.size(); ++r)
-                std::memcpy(&table[r * ref_len], refs[r].data(), ref_len);
-            check(drm_refs_create((const uint8_t *)table.data(), (int64_t)refs.size(), (int32_t)ref_len,
-                                  (int64_t)ref_len, device, &rt));
-            size_t qs = 0;
-            for (auto &q : qseqs)
-                qs = std::max(qs, q.size());
-            std::string qbuf(nq * qs, '\0');
-            std::vector<int32_t> ql(nq);
-            for (size_t i = 0; i < nq; ++i) {
-                std::memcpy(&qbuf[i * qs], qseqs[i].data(), qseqs[i].size());
-                ql[i] = (int32_t)qseqs[i].size();
-            }
-            sw_scores.assign(nq * (size_t)k, -1);
-            sw_ids.assign(nq * (size_t)k, ~0ull);
-            std::vector<int32_t> counts(nq);
-            int64_t bad = -1;
-            int rc = drm_post_process_sw_static(rt, I.data(), (int64_t)nq, k_clusters, (const uint8_t *)qbuf.data(),
-                                                ql.data(), (int32_t)qs, (int64_t)stride, k, k_clusters,
-                                                sw_scores.data(), sw_ids.data(), counts.data(), &bad);
+        int rc;
+        if (multi)
+            rc = drm_multi_search_rerank(multi, x.p, (int64_t)nq, (int32_t)dim, k_clusters, ef, is_npy ? nullptr : qbuf.p,
+                                         ql.p, (int32_t)qs, (int64_t)stride, k, D.p, I.p, sw_scores.p, sw_ids.p, status.p,
+                                         &st);
+        else
+            rc = drm_search_rerank(index, rt, x.p, (int64_t)nq, (int32_t)dim, k_clusters, ef, is_npy ? nullptr : qbuf.p,
+                                   ql.p, (int32_t)qs, (int64_t)stride, k, D.p, I.p, sw_scores.p, sw_ids.p, status.p, &st);
+        const std::string err = rc == DRM_OK ? "" : drm_last_error();
+        if (rt)
             drm_refs_free(rt);
-            check(rc);
-            std::cout << "[MAIN] Post-processing (SW rerank) time: " << ms_since(t0) << " ms" << std::endl;
-        }
+        if (index)
+            drm_index_free(index);
+        if (multi)
+            drm_multi_free(multi);
+        if (rc != DRM_OK)
+            throw drm::Error(rc, err);
+        std::cout << "[MAIN] Search" << (is_npy ? "" : " + SW rerank") << " time: " << ms_since(t0) << " ms (device "
+                  << st.kernel_ms << " ms, ndis " << st.ndis << ", nhops " << st.nhops << ", " << devices.size()
+                  << " device(s))" << std::endl;
+        if (!is_npy) // rows of a query with no candidate at all (reranker.cpp:10-11) stay -1 / 2^64-1
+            for (size_t i = 0; i < nq; ++i)
+                for (int j = std::max(status.p[i], 0); j < k; ++j) {
+                    sw_scores.p[i * (size_t)k + (size_t)j] = -1;
+                    sw_ids.p[i * (size_t)k + (size_t)j] = ~0ull;
+                }
 
         // ---- outputs (save_results, src/utils/utils.cpp:264-334)
         t0 = clk::now();
@@ -200,14 +255,14 @@ int main(int argc, char *argv[])
         std::vector<float> dis(nq * kout);
         for (size_t i = 0; i < nq; ++i)
             for (size_t j = 0; j < kout; ++j) {
-                idx[i * kout + j] = (uint64_t)I[i * k_clusters + j];
-                dis[i * kout + j] = D[i * k_clusters + j];
+                idx[i * kout + j] = (uint64_t)I.p[i * k_clusters + j];
+                dis[i * kout + j] = D.p[i * k_clusters + j];
             }
         drm::npy_save(out_dir + "/indices.npy", idx.data(), {nq, kout}, 'u', 8);
         drm::npy_save(out_dir + "/distances.npy", dis.data(), {nq, kout}, 'f', 4);
-        if (!sw_scores.empty()) {
-            drm::npy_save(out_dir + "/sw_scores.npy", sw_scores.data(), {nq, (size_t)k}, 'i', 4);
-            drm::npy_save(out_dir + "/sw_ids.npy", sw_ids.data(), {nq, (size_t)k}, 'u', 8);
+        if (!is_npy) {
+            drm::npy_save(out_dir + "/sw_scores.npy", sw_scores.p, {nq, (size_t)k}, 'i', 4);
+            drm::npy_save(out_dir + "/sw_ids.npy", sw_ids.p, {nq, (size_t)k}, 'u', 8);
         }
         std::cout << "[MAIN] Output saving time: " << ms_since(t0) << " ms" << std::endl;
         std::cout << "[MAIN] Total pipeline time: " << ms_since(master) << " ms" << std::endl;
