@@ -37,7 +37,11 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
         uint64_t o = ((uint64_t)hi << 32) | lo;
         v = o < v ? o : v;
     }
-    return v;
+    // every lane holds the minimum now; readfirstlane tells the compiler so (a shuffle result is a
+    // divergent value to its uniformity analysis, and branches on it would become exec-masked)
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane == 0 ? 0ull : (~0ull >> (64 - lane)); }
