@@ -276,6 +276,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     return cnt;
 }
 
+#ifndef DRM_PQ_SPEC
+#define DRM_PQ_SPEC 1 // codes + visited words of the predicted next row loaded one hop ahead
+#endif
+
 #define DRM_FSTAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -368,6 +372,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         int clear_n = 1;
         int nstep = 0, ndis0 = 0;
         int32_t pred = -1, v1_pref = -1;
+        // one hop ahead (DRM_PQ_SPEC): the codes of the predicted row's links and their visited-bitmap
+        // words, loaded with plain L2 loads at the end of the previous hop. Exact: only this wave marks
+        // its bitmap, its marks of that hop were issued before the predicted row's load (VMEM completes
+        // in order and these loads depend on that row), and nothing marks between here and their use.
+        bool spec = false;
+        uint2 c8_pref = make_uint2(0u, 0u);
+        uint32_t vw_pref = 0u;
         while (nvalid > 0) {
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
@@ -403,7 +414,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 
             // expand v0's level-0 row (one coalesced load, lane j = link j)
             int32_t v1 = v1_pref;
-            if (v0 != pred)
+            const bool hit = v0 == pred;
+            if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
             const uint64_t negm = ballot(lane < deg0 && v1 < 0);
             const int jmax = negm ? __builtin_ctzll(negm) : deg0;
@@ -411,7 +423,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             uint2 c8 = make_uint2(0u, 0u);
             uint32_t old = 0xFFFFFFFFu;
             const uint32_t bit = 1u << (v1 & 31);
-            if (act) {
+            const bool use_spec = DRM_PQ_SPEC && hit && spec;
+            if (use_spec) {
+                c8 = c8_pref;
+                old = act ? vw_pref : 0xFFFFFFFFu;
+            } else if (act) {
                 c8 = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1 * 8); // overlaps the visited test
                 old = vis_test_set(&vis[v1 >> 5], bit);
             }
@@ -423,6 +439,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         fresh = false;
                 }
             }
+            if (use_spec && fresh) // the test was a load: mark the fresh links (non-returning atomics)
+                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             DRM_FSTAMP(3);
             const uint64_t fm = ballot(fresh);
             const int nf = __builtin_popcountll(fm);
@@ -509,6 +527,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 logn += na;
             }
             nstep++;
+            spec = false;
+            if (DRM_PQ_SPEC && pred >= 0) {
+                const uint64_t pneg = ballot(lane < deg0 && v1_pref < 0);
+                const int pmax = pneg ? __builtin_ctzll(pneg) : deg0;
+                if (lane < pmax) {
+                    c8_pref = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1_pref * 8);
+                    vw_pref = __hip_atomic_load(&vis[v1_pref >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // L2, not L1
+                }
+                spec = true;
+            }
             DRM_FSTAMP(5);
         }
         DRM_FSTAMP(2);

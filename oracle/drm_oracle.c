@@ -450,6 +450,36 @@ static inline uint32_t pq_decode(const uint8_t *code, int m, int nbits)
     return (uint32_t)((acc >> shift) & ((1ull << nbits) - 1));
 }
 
+/* Sum order of one LUT entry ||x_m - c||^2 over the dsub dims (oracle_set_lut_order). faiss computes it
+ * with fvec_L2sqr under FAISS_PRAGMA_IMPRECISE_LOOP, so the order is whatever the compiler's
+ * vectorizer makes of it on the build host (the reference builds with -march=native, build.zig:48-57):
+ *   0 (default, the GPU kernel's): sequential, mul then add, no FMA;
+ *   1: 8 AVX2 lanes, lane i sums dims i, i+8, ... with FMA, then the tree (i, i+4), (i, i+2), (0, 1);
+ *   2: 16 AVX-512 lanes with FMA, then the tree 16 -> 8 -> 4 -> 2 -> 1;
+ *   3: 8 AVX2 lanes without FMA (mul, add), same tree as 1.
+ * Orders 1-3 bound how far a faiss build on an AVX2 / AVX-512 host can move from order 0. */
+static int g_lut_order = 0;
+void oracle_set_lut_order(int order) { g_lut_order = order; }
+
+static float l2_lanes(const float *x, const float *y, int d, int lanes, int fma_on)
+{
+    float acc[16] = {0};
+    for (int j = 0; j < d; j += lanes)
+        for (int i = 0; i < lanes && j + i < d; ++i) {
+            float t = x[j + i] - y[j + i];
+            if (fma_on)
+                acc[i] = fmaf(t, t, acc[i]);
+            else {
+                float sq = t * t;
+                acc[i] = acc[i] + sq;
+            }
+        }
+    for (int w = lanes / 2; w >= 1; w /= 2)
+        for (int i = 0; i < w; ++i)
+            acc[i] = acc[i] + acc[i + w];
+    return acc[0];
+}
+
 void oracle_pq_distance_table(const oracle_hnswpq_t *ix, const float *x, float *lut)
 {
     const int M = ix->pq_M, ksub = ix->ksub, dsub = ix->dsub;
@@ -458,11 +488,18 @@ void oracle_pq_distance_table(const oracle_hnswpq_t *ix, const float *x, float *
         for (int c = 0; c < ksub; ++c) {
             const float *cen = ix->centroids + ((size_t)m * ksub + c) * dsub;
             float acc = 0.0f;
-            for (int t = 0; t < dsub; ++t) {
-                float diff = xs[t] - cen[t];
-                float sq = diff * diff;
-                acc = acc + sq;
-            }
+            if (g_lut_order == 1)
+                acc = l2_lanes(xs, cen, dsub, 8, 1);
+            else if (g_lut_order == 2)
+                acc = l2_lanes(xs, cen, dsub, 16, 1);
+            else if (g_lut_order == 3)
+                acc = l2_lanes(xs, cen, dsub, 8, 0);
+            else
+                for (int t = 0; t < dsub; ++t) {
+                    float diff = xs[t] - cen[t];
+                    float sq = diff * diff;
+                    acc = acc + sq;
+                }
             lut[(size_t)m * ksub + c] = acc;
         }
     }

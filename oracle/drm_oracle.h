@@ -60,6 +60,8 @@ typedef struct {
 /* ProductQuantizer::compute_distance_table: lut[m*ksub + c] = sum_t (x[m*dsub+t]-C[m][c][t])^2,
  * summed t = 0..dsub-1 sequentially, products and sums rounded separately (no FMA). */
 void oracle_pq_distance_table(const oracle_hnswpq_t *ix, const float *x, float *lut);
+/* LUT sum order variant (0 = default sequential; 1 AVX2+FMA, 2 AVX-512+FMA, 3 AVX2 no FMA) */
+void oracle_set_lut_order(int order);
 
 /* IndexHNSW::search for n queries. D [n x k] float, I [n x k] int64, per-query ndis / nhops
  * (HNSWStats as accumulated by HNSW::search). nthreads <= 0 -> all OpenMP threads. */

@@ -50,19 +50,38 @@ struct Flat {
 
 #pragma GCC push_options
 #pragma GCC optimize("fp-contract=off")
-float l2_avx(const float *x, const float *y, int d)
+// Sum order (oracle_set_l2_order), the hnswlib kernels a -march=native build (build.zig:48-57) can pick:
+//   0 (default, the GPU kernel's): L2SqrSIMD16ExtAVX, 8 accumulators, mul then add;
+//   1: L2SqrSIMD16ExtAVX with the mul/add pair contracted to FMA (GCC contracts intrinsics);
+//   2: L2SqrSIMD16ExtAVX512, 16 accumulators, mul then add, TmpRes[0] + ... + TmpRes[15];
+//   3: L2SqrSIMD16ExtAVX512 with FMA.
+int g_l2_order = 0;
+float l2_lanes(const float *x, const float *y, int d, int lanes, bool fma_on)
 {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < d; j += 8)
-        for (int i = 0; i < 8; ++i) {
+    float acc[16] = {0};
+    for (int j = 0; j < d; j += lanes)
+        for (int i = 0; i < lanes; ++i) {
             const float t = x[j + i] - y[j + i];
-            const float sq = t * t;
-            acc[i] = acc[i] + sq;
+            if (fma_on) {
+                acc[i] = std::fma(t, t, acc[i]);
+            } else {
+                const float sq = t * t;
+                acc[i] = acc[i] + sq;
+            }
         }
     float r = acc[0];
-    for (int i = 1; i < 8; ++i)
+    for (int i = 1; i < lanes; ++i)
         r = r + acc[i];
     return r;
+}
+float l2_avx(const float *x, const float *y, int d)
+{
+    switch (g_l2_order) {
+    case 1: return l2_lanes(x, y, d, 8, true);
+    case 2: return l2_lanes(x, y, d, 16, false);
+    case 3: return l2_lanes(x, y, d, 16, true);
+    default: return l2_lanes(x, y, d, 8, false);
+    }
 }
 #pragma GCC pop_options
 
@@ -183,6 +202,8 @@ void search_one(const Flat &ix, const float *q, int k, int ef_, float *D, int64_
 } // namespace
 
 extern "C" {
+void oracle_set_l2_order(int order) { g_l2_order = order; }
+
 
 static size_t g_maxcand = 0;
 static int64_t g_tieq[3] = {0, 0, 0};

@@ -154,6 +154,16 @@ def pq_distance_table(fx_or_struct, x):
     return lut.reshape(s.pq_M, s.ksub)
 
 
+def set_lut_order(order):
+    """faiss LUT sum order variant of the oracle (drm_oracle.c oracle_set_lut_order); 0 = default."""
+    lib().oracle_set_lut_order(C.c_int(int(order)))
+
+
+def set_l2_order(order):
+    """hnswlib L2 kernel variant of the oracle (hnswlib_oracle.cpp oracle_set_l2_order); 0 = default."""
+    hnswlib_lib().oracle_set_l2_order(C.c_int(int(order)))
+
+
 def hnswlib_lib():
     global _hl
     if _hl is None:
