@@ -65,6 +65,24 @@ def committed_pmc(kernel_substr, workload):
     return None, None
 
 
+VALU_CYC = 2.4  # cycles per wave64 32-bit VALU instruction per SIMD at >= 4 waves (profiles/r02/valu_rate_probe.txt)
+
+
+def issue_ceiling(pmc, hops, ms):
+    """Issue-bound ceiling of the search kernel from its committed PMC counters: wave-instructions per
+    hop, and the launch time the VALU stream alone (1024 SIMDs at VALU_CYC cycles per instruction) and
+    the scalar stream alone (one scalar unit per CU, 256 CUs, one instruction per cycle) would take."""
+    if not pmc or "SQ_INSTS_VALU" not in pmc or hops <= 0:
+        return None
+    v, sc, lds = pmc["SQ_INSTS_VALU"], pmc.get("SQ_INSTS_SALU", 0.0), pmc.get("SQ_INSTS_LDS", 0.0)
+    valu_ms = v * VALU_CYC / (1024 * CLOCK_HZ) * 1e3
+    salu_ms = sc / (256 * CLOCK_HZ) * 1e3
+    return {"valu_per_hop": round(v / hops, 1), "salu_per_hop": round(sc / hops, 1), "lds_per_hop": round(lds / hops, 1),
+            "valu_bound_ms": round(valu_ms, 2), "salu_bound_ms": round(salu_ms, 2),
+            "frac_of_issue_ceiling": round(max(valu_ms, salu_ms) / ms, 3),
+            "note": "PMC from the committed profile of this workload; hops = this run's measured nhops"}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -271,11 +289,12 @@ def run_c4(args, D):
     w = synth.Workload("c4", 20_000_299, N * Q, stride=4, seed=43, read_seed=8)
     if D.rank == 0:
         t0 = time.time()
-        w.generate(args.cache, nthreads=args.build_threads, log=log, need_refs=False)
+        w.generate(args.cache, nthreads=args.build_threads, log=log, need_refs=False, gpu_build=True,
+                   device=D.local_rank % max(ndev, 1))
         log(f"[bench] C4 workload ready in {time.time() - t0:.1f}s: index {w.index_path}")
     D.barrier()
     if D.rank != 0:
-        w.generate(args.cache, need_refs=False)
+        w.generate(args.cache, need_refs=False, gpu_build=True)
     lo, hi = shard_range(N * Q, D.rank, N)
     q_emb = np.ascontiguousarray(w.q_emb[lo:hi])
     ix = HnswPqIndex(w.index_path, D.local_rank % max(ndev, 1))
@@ -332,7 +351,7 @@ def run_c4(args, D):
             "vs_baseline": None, "dtype": "fp32 (PQ-ADC distances)",
             "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
             "config": {"workload": "C4: synthetic 20 Mbp genome, stride-4 sparse IndexHNSWPQ of "
-                                   f"{info.ntotal} windows (M_pq=8 nbits=8 M_hnsw=16 EFC=200), search only",
+                                   f"{info.ntotal} windows (M_pq=8 nbits=8 M_hnsw=16 EFC=200, GPU-built), search only",
                        "n_refs": int(info.ntotal), "queries_per_gpu": Q, "ef": args.ef, "k": args.k,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
             "roofline": {"bound": "hbm", "kernel": SEARCH_KERNEL, "achieved": round(r["achieved"], 2),
@@ -524,7 +543,8 @@ def main():
                                             "read correction, uncalibrated for 4-8 B random reads")
                          if traffic is not None else None,
                          "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
-                         if pmc and "valu_issue_frac" in pmc else None},
+                         if pmc and "valu_issue_frac" in pmc else None,
+                         "issue": issue_ceiling(pmc, float(nhops.sum()), search_ms)},
             "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_gcups, 1),
                             "peak": round(sw_peak_gcups, 1), "unit": "GCUPS",
                             "frac": round(sw_gcups / sw_peak_gcups, 4),

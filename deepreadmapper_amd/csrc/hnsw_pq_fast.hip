@@ -63,6 +63,27 @@ __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // la
     return ((uint64_t)h << 32) | o;
 }
 
+#ifndef DRM_PQ_VPATH
+#define DRM_PQ_VPATH 1 // pop128's sift-down path by per-lane ancestor masks (0: scalar walk)
+#endif
+
+// Per-lane constants of node p = lane: A = p and its ancestors, Aup = its ancestors, Lreq = the
+// ancestors whose path toward p takes the left child (2a + 1).
+struct PathConst {
+    uint64_t A, Aup, Lreq;
+    __device__ explicit PathConst(int lane) : A(1ull << lane), Aup(0), Lreq(0)
+    {
+        for (int c = lane; c > 0;) {
+            const int a = (c - 1) >> 1;
+            A |= 1ull << a;
+            Aup |= 1ull << a;
+            if (c & 1)
+                Lreq |= 1ull << a;
+            c = a;
+        }
+    }
+};
+
 // MinimaxHeap arrays (ef <= 128) in the sibling-pair layout.
 struct Heap {
     uint64_t L, R;
@@ -114,7 +135,7 @@ struct Heap {
     // path is walked on the scalar unit over two ballots (which child each node takes, whether it
     // moves up) -- a few SALU cycles per level instead of a chain of cross-lane round trips -- while
     // the one ds_bpermute that fetches the moving values is already in flight.
-    __device__ __forceinline__ void pop128(int lane)
+    __device__ __forceinline__ void pop128(int lane, const PathConst &pc)
     {
         const uint64_t val = readlane64(L, 63);
         const bool takeL = lane == 63 || L > R;
@@ -122,6 +143,18 @@ struct Heap {
         const uint64_t chv = takeL ? L : R;
         const uint64_t up = bperm64(chv, ch & 63);
         const uint64_t lm = ballot(takeL), mv = ballot(!(val > chv));
+#if DRM_PQ_VPATH
+        // node p is on the sift-down path (its chosen child moves up) iff p and all its ancestors have
+        // mv set and every ancestor chose the child toward p: one test per lane against its constant
+        // ancestor masks, instead of a 7-step scalar walk
+        const bool inW = (mv & pc.A) == pc.A && (lm & pc.Aup) == pc.Lreq;
+        const uint64_t W = ballot(inW);
+        uint32_t hole = 0;
+        if (W) {
+            const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
+            hole = 2u * last + 2u - (uint32_t)((lm >> last) & 1ull);
+        }
+#else
         uint64_t W = 0;
         uint32_t hole = 0;
 #pragma unroll
@@ -131,6 +164,7 @@ struct Heap {
             W |= 1ull << hole;
             hole = 2u * hole + 2u - (uint32_t)((lm >> hole) & 1ull);
         }
+#endif
         const bool writer = (W >> lane) & 1ull;
         const uint64_t nv = (uint32_t)ch == hole ? val : up;
         if (writer && takeL)
@@ -305,6 +339,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
     const int ef = a.ef, k = a.k, deg0 = a.deg0;
+    const PathConst pconst(lane);
     const uint32_t kInfKey = ord32(INFINITY);
 
     for (;;) {
@@ -496,7 +531,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (lo32(root) != kPopLo)
                         --nvalid;
                     if (ef == 128) {
-                        hp.pop128(lane);
+                        hp.pop128(lane, pconst);
                         hp.push128(val, lane);
                     } else {
                         hp.pop(kc, lane);
