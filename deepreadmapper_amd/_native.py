@@ -33,7 +33,9 @@ EXPORTS = [
     "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_fallbacks",
     "drm_refs_get_info", "drm_host_alloc", "drm_host_free", "drm_search_rerank", "drm_multi_create",
     "drm_multi_free", "drm_multi_get_index_info", "drm_multi_search_rerank", "drm_comm_unique_id", "drm_comm_init",
-    "drm_comm_free", "drm_comm_gather_rows",
+    "drm_comm_free", "drm_comm_gather_rows", "drm_refs_create_genome", "drm_refs_is_genome",
+    "drm_extract_fasta_sequence", "drm_post_process_sw_dynamic", "drm_post_process_sw_dynamic_device",
+    "drm_multi_create_genome",
 ]
 
 
@@ -135,6 +137,14 @@ def lib():
         "drm_comm_init": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
         "drm_comm_free": (C.c_int, [vp]),
         "drm_comm_gather_rows": (C.c_int, [vp, vp, i64, i64, vp, C.c_int, vp]),
+        "drm_refs_create_genome": (C.c_int, [vp, i64, i32, C.c_int, C.POINTER(vp)]),
+        "drm_refs_is_genome": (C.c_int, [vp, C.POINTER(C.c_int)]),
+        "drm_multi_create_genome": (C.c_int, [C.c_char_p, vp, C.c_int, vp, i64, i32, C.POINTER(vp)]),
+        "drm_extract_fasta_sequence": (C.c_int, [C.c_char_p, vp, C.POINTER(i64)]),
+        "drm_post_process_sw_dynamic": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
+                                                  C.POINTER(i64)]),
+        "drm_post_process_sw_dynamic_device": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
+                                                         vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

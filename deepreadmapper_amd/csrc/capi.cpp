@@ -12,6 +12,7 @@
 #include "drm_device.h"
 
 namespace drm {
+void exec_release(const void *index); // exec.cpp
 static thread_local std::string g_last_error;
 void set_last_error(const std::string &msg) { g_last_error = msg; }
 } // namespace drm
@@ -264,6 +265,7 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.nbr0 = upload_vec(nbr0, d.device_bytes);
             d.upper_off = upload_vec(upper_off, d.device_bytes);
             d.upper_nbr = upload_vec(upper, d.device_bytes);
+            drm::reserve_search_scratch(d); // the per-slot search workspace, once, outside any search
         } catch (...) {
             free_index(d);
             throw;
@@ -283,6 +285,7 @@ int drm_index_load(const char *path, int device, drm_index **out)
 
 int drm_index_free(drm_index *index)
 {
+    drm::exec_release(index);
     return guarded([&] {
         if (!index)
             return;
@@ -699,6 +702,38 @@ int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int6
     });
 }
 
+int drm_refs_create_genome(const uint8_t *genome, int64_t len, int32_t ref_len, int device, drm_refs **out)
+{
+    return guarded([&] {
+        if (!out || (!genome && len > 0))
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (len < 0 || ref_len < 0)
+            throw Error(DRM_ERR_ARG, "invalid genome / ref_len");
+        if (len >= ((int64_t)1 << 31))
+            throw Error(DRM_ERR_UNSUPPORTED, "genomes of 2^31 bases or more are not supported (32-bit window ids)");
+        DRM_HIP_CHECK(hipSetDevice(device));
+        std::unique_ptr<drm_refs> r(new drm_refs());
+        r->dev.device = device;
+        r->dev.ref_len = ref_len;
+        r->dev.row_stride = 16;
+        r->dev.glen = len;
+        r->dev.n_ref = len >= ref_len ? 2 * (len - ref_len + 1) : 0;
+        DRM_HIP_CHECK(hipMalloc(&r->dev.genome, (size_t)std::max<int64_t>(len, 1)));
+        if (len > 0)
+            DRM_HIP_CHECK(hipMemcpy(r->dev.genome, genome, (size_t)len, hipMemcpyHostToDevice));
+        *out = r.release();
+    });
+}
+
+int drm_refs_is_genome(const drm_refs *refs, int *is_genome)
+{
+    return guarded([&] {
+        if (!refs || !is_genome)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *is_genome = refs->dev.genome ? 1 : 0;
+    });
+}
+
 int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device)
 {
     return guarded([&] {
@@ -720,7 +755,7 @@ int drm_refs_free(drm_refs *refs)
             return;
         (void)hipSetDevice(refs->dev.device);
         for (void *p : {(void *)refs->dev.windows, (void *)refs->dev.ws_ids, (void *)refs->dev.ws_scores,
-                        (void *)refs->dev.ws_ncand})
+                        (void *)refs->dev.ws_ncand, (void *)refs->dev.genome})
             if (p)
                 (void)hipFree(p);
         delete refs;
@@ -740,6 +775,8 @@ static drm::RerankArgs make_rerank_args(drm_refs *refs, const int64_t *nb, int64
     if ((int64_t)k > (int64_t)k_clusters * 2 * stride) // post_processor.cpp:486-489
         throw Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
     drm::RerankArgs a{};
+    a.genome = refs->dev.genome;
+    a.glen = refs->dev.glen;
     a.refs = refs->dev.windows;
     a.n_ref = refs->dev.n_ref;
     a.ref_len = refs->dev.ref_len;
@@ -759,12 +796,23 @@ static drm::RerankArgs make_rerank_args(drm_refs *refs, const int64_t *nb, int64
     return a;
 }
 
-int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
-                                      const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
-                                      int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
-                                      uint64_t *d_top_ids, int32_t *d_status, void *stream)
+static void require_mode(const drm_refs *refs, bool dynamic)
+{
+    if (!refs)
+        throw Error(DRM_ERR_ARG, "null refs");
+    if (dynamic && !refs->dev.genome)
+        throw Error(DRM_ERR_ARG, "post_process_sw_dynamic needs a genome handle (drm_refs_create_genome)");
+    if (!dynamic && refs->dev.genome)
+        throw Error(DRM_ERR_ARG, "post_process_sw_static needs a window table (drm_refs_create), not a genome");
+}
+
+static int post_process_device(bool dynamic, drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                               const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride, int64_t stride,
+                               int32_t k, int32_t k_clusters, int32_t *d_top_scores, uint64_t *d_top_ids,
+                               int32_t *d_status, void *stream)
 {
     return guarded([&] {
+        require_mode(refs, dynamic);
         drm::RerankArgs a = make_rerank_args(refs, d_neighbors, nq, kk, d_queries, d_q_len, q_stride, stride, k,
                                              k_clusters, d_top_scores, d_top_ids, d_status);
         DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
@@ -773,12 +821,31 @@ int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors
     });
 }
 
-int drm_post_process_sw_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
-                               const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
-                               int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
-                               int32_t *counts, int64_t *bad_query)
+int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                                      int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
+                                      uint64_t *d_top_ids, int32_t *d_status, void *stream)
+{
+    return post_process_device(false, refs, d_neighbors, nq, kk, d_queries, d_q_len, q_stride, stride, k, k_clusters,
+                               d_top_scores, d_top_ids, d_status, stream);
+}
+
+int drm_post_process_sw_dynamic_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                       const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                                       int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
+                                       uint64_t *d_top_ids, int32_t *d_status, void *stream)
+{
+    return post_process_device(true, refs, d_neighbors, nq, kk, d_queries, d_q_len, q_stride, stride, k, k_clusters,
+                               d_top_scores, d_top_ids, d_status, stream);
+}
+
+static int post_process_host(bool dynamic, drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                             const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                             int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids, int32_t *counts,
+                             int64_t *bad_query)
 {
     return guarded([&] {
+        require_mode(refs, dynamic);
         if (bad_query)
             *bad_query = -1;
         if (nq <= 0)
@@ -834,22 +901,42 @@ int drm_post_process_sw_static(drm_refs *refs, const int64_t *neighbors, int64_t
             // count the candidates of the offending query for the reference's message
             const int64_t *nb = neighbors + first_bad * kk;
             int64_t nc = 0;
+            // static lookup checks ids against the window count, dynamic against the genome length
+            const uint64_t limit = dynamic ? (uint64_t)refs->dev.glen : (uint64_t)refs->dev.n_ref;
             for (int i = 0; i < std::min(k_clusters, kk); ++i) {
                 uint64_t id = (uint64_t)nb[i];
                 if (stride == 1) {
-                    nc += id < (uint64_t)refs->dev.n_ref;
+                    nc += dynamic || id < limit;
                 } else {
                     uint64_t act = id * (uint64_t)stride;
-                    if (act >= (uint64_t)refs->dev.n_ref)
+                    if (act >= limit)
                         continue;
                     uint64_t s0 = act >= (uint64_t)(stride - 1) ? act - stride + 1 : 0;
-                    nc += (int64_t)(std::min<uint64_t>(act + stride, refs->dev.n_ref) - s0);
+                    nc += (int64_t)(std::min<uint64_t>(act + stride, limit) - s0);
                 }
             }
             throw Error(DRM_ERR_CANDS,
                         "Not enough candidates (" + std::to_string(nc) + " < " + std::to_string(k) + ")");
         }
     });
+}
+
+int drm_post_process_sw_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                               int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
+                               int32_t *counts, int64_t *bad_query)
+{
+    return post_process_host(false, refs, neighbors, nq, kk, queries, q_len, q_stride, stride, k, k_clusters,
+                             top_scores, top_ids, counts, bad_query);
+}
+
+int drm_post_process_sw_dynamic(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                                const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                                int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
+                                int32_t *counts, int64_t *bad_query)
+{
+    return post_process_host(true, refs, neighbors, nq, kk, queries, q_len, q_stride, stride, k, k_clusters,
+                             top_scores, top_ids, counts, bad_query);
 }
 
 } // extern "C"

@@ -95,6 +95,7 @@ struct SearchArgs {
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc);
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream);
 
+void reserve_search_scratch(DeviceIndex &ix);
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
@@ -194,6 +195,10 @@ struct DeviceRefs {
     int32_t *ws_scores = nullptr;
     int32_t *ws_ncand = nullptr;
     size_t ws_elems = 0, ws_nq = 0;
+    // dynamic lookup (use_dynamic, post_process_sw_dynamic): the genome string instead of a window
+    // table; window id w is genome[w / 2 ..+ ref_len), reverse-complemented when w is odd
+    uint8_t *genome = nullptr;
+    int64_t glen = 0;
 };
 
 struct RerankArgs {
@@ -212,6 +217,9 @@ struct RerankArgs {
     int32_t *top_scores;
     uint64_t *top_ids;
     int32_t *status;
+    // dynamic lookup (post_process_sw_dynamic): genome != nullptr replaces the window table
+    const uint8_t *genome;
+    int64_t glen;
     // workspace (set by launch_sw_rerank)
     int32_t cmax;
     uint64_t *cand_ids;

@@ -118,6 +118,15 @@ void format_fastq(const std::string &data, std::vector<std::string> &seqs, std::
 void read_file(const std::string &path, std::vector<std::string> &seqs, std::vector<std::string> &ids,
                size_t ref_len = 150, size_t stride = 1, bool lookup_mode = false);
 std::string read_whole_file(const std::string &path);
+// extract_FASTA_sequence (parse_inputs.cpp:174-220): skip the first line, keep the upper-cased
+// A/C/G/T/N letters of everything after it (later header lines included), drop the rest.
+std::string extract_fasta_sequence(const std::string &path);
+// write_sam / write_sam_streaming (utils.cpp:336-503) for one block of queries: the SAM lines of
+// queries [q0, q0 + nq) whose ids[i][0 .. counts[i]) are dense window ids (ids[i] at ids + i * k).
+// `header` writes @HD / @SQ first (SN ref_name, LN ref_len: the reference's quirk) and truncates.
+void write_sam_block(const std::string &path, bool header, const std::string &ref_name, size_t ref_len,
+                     const std::vector<std::string> &query_seqs, const std::vector<std::string> &query_ids,
+                     size_t q0, size_t nq, const uint64_t *ids, const int32_t *counts, size_t k);
 
 void build_hnswpq(const float *x, int64_t n, int d, int M_pq, int nbits, int M_hnsw, int efc, double sample_rate,
                   int nthreads, uint64_t seed, const std::string &path);

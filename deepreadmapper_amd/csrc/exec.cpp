@@ -18,9 +18,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -76,19 +80,112 @@ struct DevMem {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
-// One device buffer set of the ping-pong pipeline.
+// One device buffer set of the batch pipeline.
 struct BatchSet {
     std::unique_ptr<DevMem> x, q, ql, D, I, nd, nh, sc, id, st;
-    hipEvent_t in_done = nullptr, comp_done = nullptr, out_done = nullptr;
-    int64_t lo = 0, n = 0; // queries of the batch in flight in this set
+    hipEvent_t in_done = nullptr, search_done = nullptr, comp_done = nullptr, out_done = nullptr;
     bool busy = false;
 };
 
-int64_t batch_size_default()
+constexpr int kSets = 3;
+
+// Streams, events and device buffers of the executor, kept per index handle between calls (an index
+// handle is single-stream, so one executor per handle never races), grown when a call needs more.
+struct ExecCache {
+    int device = -1;
+    hipStream_t s_in = nullptr, s_search = nullptr, s_sw = nullptr, s_out = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    BatchSet sets[kSets];
+    int64_t B = 0, d = 0, kc = 0, kr = 0, q_stride = 0;
+    bool rr = false;
+
+    void init(int dev)
+    {
+        device = dev;
+        HC(hipSetDevice(dev));
+        for (hipStream_t *s : {&s_in, &s_search, &s_sw, &s_out})
+            HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        HC(hipEventCreate(&e0));
+        HC(hipEventCreate(&e1));
+        for (auto &b : sets)
+            for (hipEvent_t *e : {&b.in_done, &b.search_done, &b.comp_done, &b.out_done})
+                HC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    void reserve(int64_t B_, int64_t d_, int64_t kc_, int64_t kr_, int64_t qs_, bool rr_)
+    {
+        if (B_ <= B && d_ == d && kc_ <= kc && kr_ <= kr && qs_ <= q_stride && (rr == rr_ || !rr_))
+            return;
+        B = std::max(B, B_);
+        d = d_;
+        kc = std::max(kc, kc_);
+        kr = std::max(kr, kr_);
+        q_stride = std::max(q_stride, qs_);
+        rr = rr || rr_;
+        for (auto &s : sets) {
+            s.x.reset(new DevMem(sizeof(float) * (size_t)B * d));
+            s.D.reset(new DevMem(sizeof(float) * (size_t)B * kc));
+            s.I.reset(new DevMem(sizeof(int64_t) * (size_t)B * kc));
+            s.nd.reset(new DevMem(sizeof(int32_t) * (size_t)B));
+            s.nh.reset(new DevMem(sizeof(int32_t) * (size_t)B));
+            if (rr) {
+                s.q.reset(new DevMem((size_t)B * std::max<int64_t>(q_stride, 1)));
+                s.ql.reset(new DevMem(sizeof(int32_t) * (size_t)B));
+                s.sc.reset(new DevMem(sizeof(int32_t) * (size_t)B * std::max<int64_t>(kr, 1)));
+                s.id.reset(new DevMem(sizeof(uint64_t) * (size_t)B * std::max<int64_t>(kr, 1)));
+                s.st.reset(new DevMem(sizeof(int32_t) * (size_t)B));
+            }
+        }
+    }
+    void drain()
+    {
+        for (hipStream_t s : {s_in, s_search, s_sw, s_out})
+            if (s)
+                (void)hipStreamSynchronize(s);
+        for (auto &b : sets)
+            b.busy = false;
+    }
+    ~ExecCache()
+    {
+        if (device < 0)
+            return;
+        (void)hipSetDevice(device);
+        drain();
+        for (auto &b : sets)
+            for (hipEvent_t e : {b.in_done, b.search_done, b.comp_done, b.out_done})
+                if (e)
+                    (void)hipEventDestroy(e);
+        for (hipEvent_t e : {e0, e1})
+            if (e)
+                (void)hipEventDestroy(e);
+        for (hipStream_t s : {s_in, s_search, s_sw, s_out})
+            if (s)
+                (void)hipStreamDestroy(s);
+    }
+};
+
+std::mutex g_exec_mu;
+// never destroyed: HIP calls from static destructors at process exit are unsafe; handles are released
+// explicitly through drm_index_free
+std::map<const void *, std::unique_ptr<ExecCache>> &g_exec = *new std::map<const void *, std::unique_ptr<ExecCache>>();
+
+ExecCache &exec_for(const drm_index *ix, int device)
+{
+    std::lock_guard<std::mutex> lk(g_exec_mu);
+    auto &p = g_exec[ix];
+    if (!p || p->device != device) {
+        p.reset(new ExecCache());
+        p->init(device);
+    }
+    return *p;
+}
+
+int64_t batch_size_for(int64_t n)
 {
     if (const char *e = std::getenv("DRM_BATCH"))
         return std::max<int64_t>(1, std::atoll(e));
-    return 262144; // ~1 GB of device buffers per set at K = 128
+    // at least four batches for the copy / compute overlap, none below 32k queries (each kernel
+    // launch drains its persistent grid at the end) nor above 256k (~1 GB of buffers per set)
+    return std::min<int64_t>(262144, std::max<int64_t>(32768, (n + 3) / 4));
 }
 
 // status -> error, as drm_post_process_sw_static reports it (reranker.cpp:26-29, post_processor.cpp:486-489)
@@ -112,7 +209,7 @@ void check_status(const int32_t *status, int64_t n, int32_t k)
 void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, int32_t d, int32_t k_clusters,
                    int32_t ef, const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
                    int32_t k, float *D, int64_t *I, int32_t *sw_scores, uint64_t *sw_ids, int32_t *status,
-                   drm_search_stats *stats, int64_t batch)
+                   drm_search_stats *stats)
 {
     if (!index || !x || !D || !I)
         throw Error(DRM_ERR_ARG, "null argument");
@@ -125,6 +222,7 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
     if (k_clusters <= 0)
         throw Error(DRM_ERR_ARG, "k must be > 0");
     const bool rr = refs != nullptr;
+    int genome_mode = 0;
     if (rr) {
         if (!queries || !q_len || !sw_scores || !sw_ids || !status)
             throw Error(DRM_ERR_ARG, "null rerank argument");
@@ -137,101 +235,84 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
                 throw Error(DRM_ERR_ARG, "query length outside [0, q_stride]");
         int dev_r = -1;
         abi_check(drm_refs_get_info(refs, nullptr, nullptr, &dev_r));
+        abi_check(drm_refs_is_genome(refs, &genome_mode));
         if (dev_r != info.device)
             throw Error(DRM_ERR_ARG, "index and window table live on different devices");
     }
-    HC(hipSetDevice(info.device));
-    const int64_t B = std::min<int64_t>(n, batch > 0 ? batch : batch_size_default());
-    const size_t kc = (size_t)k_clusters, kr = rr ? (size_t)k : 0;
-    hipStream_t s_in, s_comp, s_out;
-    HC(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking));
-    HC(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
-    std::vector<BatchSet> sets(n > B ? 2 : 1);
-    std::vector<int32_t> nd_host((size_t)n), nh_host((size_t)n);
-    hipEvent_t e0, e1;
-    HC(hipEventCreate(&e0));
-    HC(hipEventCreate(&e1));
-    auto cleanup = [&] {
-        (void)hipStreamSynchronize(s_in);
-        (void)hipStreamSynchronize(s_comp);
-        (void)hipStreamSynchronize(s_out);
-        for (auto &s : sets)
-            for (hipEvent_t e : {s.in_done, s.comp_done, s.out_done})
-                if (e)
-                    (void)hipEventDestroy(e);
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        (void)hipStreamDestroy(s_in);
-        (void)hipStreamDestroy(s_comp);
-        (void)hipStreamDestroy(s_out);
+    static const bool verbose = std::getenv("DRM_EXEC_VERBOSE") && std::atoi(std::getenv("DRM_EXEC_VERBOSE"));
+    const auto t_start = std::chrono::steady_clock::now();
+    auto ms_since = [&] {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     };
+    HC(hipSetDevice(info.device));
+    const int64_t B = std::min<int64_t>(n, batch_size_for(n));
+    const size_t kc = (size_t)k_clusters, kr = rr ? (size_t)k : 0;
+    ExecCache &ex = exec_for(index, info.device);
+    std::vector<int32_t> nd_host((size_t)n), nh_host((size_t)n);
     try {
-        for (auto &s : sets) {
-            s.x.reset(new DevMem(sizeof(float) * (size_t)B * d));
-            s.D.reset(new DevMem(sizeof(float) * (size_t)B * kc));
-            s.I.reset(new DevMem(sizeof(int64_t) * (size_t)B * kc));
-            s.nd.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-            s.nh.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-            if (rr) {
-                s.q.reset(new DevMem((size_t)B * q_stride));
-                s.ql.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-                s.sc.reset(new DevMem(sizeof(int32_t) * (size_t)B * kr));
-                s.id.reset(new DevMem(sizeof(uint64_t) * (size_t)B * kr));
-                s.st.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-            }
-            HC(hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming));
-            HC(hipEventCreateWithFlags(&s.comp_done, hipEventDisableTiming));
-            HC(hipEventCreateWithFlags(&s.out_done, hipEventDisableTiming));
-        }
-        HC(hipEventRecord(e0, s_comp));
+        ex.reserve(B, d, (int64_t)kc, (int64_t)kr, rr ? q_stride : 0, rr);
+        if (verbose)
+            std::fprintf(stderr, "[exec] %lld queries, batch %lld: setup %.2f ms\n", (long long)n, (long long)B, ms_since());
+        HC(hipEventRecord(ex.e0, ex.s_search));
         int64_t b = 0;
         for (int64_t lo = 0; lo < n; lo += B, ++b) {
-            BatchSet &s = sets[(size_t)(b % (int64_t)sets.size())];
+            BatchSet &s = ex.sets[b % kSets];
             if (s.busy) // the set's previous batch has left the device
                 HC(hipEventSynchronize(s.out_done));
-            s.lo = lo;
-            s.n = std::min(B, n - lo);
             s.busy = true;
-            const size_t m = (size_t)s.n;
-            // host -> device (stream s_in)
-            HC(hipMemcpyAsync(s.x->p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, s_in));
+            const int64_t nb = std::min(B, n - lo);
+            const size_t m = (size_t)nb;
+            // host -> device (s_in)
+            HC(hipMemcpyAsync(s.x->p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_in));
             if (rr) {
-                HC(hipMemcpyAsync(s.q->p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice, s_in));
-                HC(hipMemcpyAsync(s.ql->p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, s_in));
+                HC(hipMemcpyAsync(s.q->p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice,
+                                  ex.s_in));
+                HC(hipMemcpyAsync(s.ql->p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_in));
             }
-            HC(hipEventRecord(s.in_done, s_in));
-            // search + rerank (stream s_comp)
-            HC(hipStreamWaitEvent(s_comp, s.in_done, 0));
-            abi_check(drm_search_device_ex(index, s.x->as<float>(), s.n, k_clusters, ef, s.D->as<float>(),
+            HC(hipEventRecord(s.in_done, ex.s_in));
+            // search (s_search), then rerank (s_sw): the next batch's search may start while this batch's
+            // rerank drains, filling the CUs its persistent grid leaves idle
+            HC(hipStreamWaitEvent(ex.s_search, s.in_done, 0));
+            abi_check(drm_search_device_ex(index, s.x->as<float>(), nb, k_clusters, ef, s.D->as<float>(),
                                            s.I->as<int64_t>(), s.nd->as<int32_t>(), s.nh->as<int32_t>(), nullptr,
-                                           s_comp));
-            if (rr)
-                abi_check(drm_post_process_sw_static_device(refs, s.I->as<int64_t>(), s.n, k_clusters,
-                                                            s.q->as<uint8_t>(), s.ql->as<int32_t>(), q_stride, stride,
-                                                            k, k_clusters, s.sc->as<int32_t>(), s.id->as<uint64_t>(),
-                                                            s.st->as<int32_t>(), s_comp));
-            HC(hipEventRecord(s.comp_done, s_comp));
-            // device -> host (stream s_out)
-            HC(hipStreamWaitEvent(s_out, s.comp_done, 0));
-            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D->p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, s_out));
-            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I->p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, s_out));
-            HC(hipMemcpyAsync(nd_host.data() + lo, s.nd->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
-            HC(hipMemcpyAsync(nh_host.data() + lo, s.nh->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
+                                           ex.s_search));
+            HC(hipEventRecord(s.search_done, ex.s_search));
+            hipStream_t s_last = ex.s_search;
+            if (rr) {
+                HC(hipStreamWaitEvent(ex.s_sw, s.search_done, 0));
+                auto *pp = genome_mode ? drm_post_process_sw_dynamic_device : drm_post_process_sw_static_device;
+                abi_check(pp(refs, s.I->as<int64_t>(), nb, k_clusters, s.q->as<uint8_t>(), s.ql->as<int32_t>(), q_stride,
+                             stride, k, k_clusters, s.sc->as<int32_t>(), s.id->as<uint64_t>(), s.st->as<int32_t>(),
+                             ex.s_sw));
+                s_last = ex.s_sw;
+            }
+            HC(hipEventRecord(s.comp_done, s_last));
+            // device -> host (s_out)
+            HC(hipStreamWaitEvent(ex.s_out, s.comp_done, 0));
+            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D->p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I->p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(nd_host.data() + lo, s.nd->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(nh_host.data() + lo, s.nh->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
             if (rr) {
                 HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc->p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
-                                  s_out));
+                                  ex.s_out));
                 HC(hipMemcpyAsync(sw_ids + (size_t)lo * kr, s.id->p, sizeof(uint64_t) * m * kr, hipMemcpyDeviceToHost,
-                                  s_out));
-                HC(hipMemcpyAsync(status + lo, s.st->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
+                                  ex.s_out));
+                HC(hipMemcpyAsync(status + lo, s.st->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
             }
-            HC(hipEventRecord(s.out_done, s_out));
+            HC(hipEventRecord(s.out_done, ex.s_out));
+            if (verbose)
+                std::fprintf(stderr, "[exec] batch %lld enqueued %.2f ms\n", (long long)b, ms_since());
         }
-        HC(hipEventRecord(e1, s_comp));
-        HC(hipStreamSynchronize(s_out));
-        HC(hipEventSynchronize(e1));
+        HC(hipStreamWaitEvent(ex.s_search, ex.sets[(b - 1) % kSets].comp_done, 0));
+        HC(hipEventRecord(ex.e1, ex.s_search));
+        HC(hipStreamSynchronize(ex.s_out));
+        HC(hipEventSynchronize(ex.e1));
+        ex.drain();
         float ms = 0.f;
-        HC(hipEventElapsedTime(&ms, e0, e1));
+        HC(hipEventElapsedTime(&ms, ex.e0, ex.e1));
+        if (verbose)
+            std::fprintf(stderr, "[exec] done %.2f ms (device span %.2f ms)\n", ms_since(), ms);
         if (stats) {
             stats->nq = n;
             stats->ndis = 0;
@@ -240,18 +321,26 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
                 stats->ndis += nd_host[(size_t)i];
                 stats->nhops += nh_host[(size_t)i];
             }
-            stats->kernel_ms = ms; // device span of the compute stream (search + rerank of all batches)
+            stats->kernel_ms = ms; // device span from the first search to the last rerank
         }
     } catch (...) {
-        cleanup();
+        ex.drain();
         throw;
     }
-    cleanup();
     if (rr)
         check_status(status, n, k);
 }
 
 } // namespace
+
+namespace drm {
+// drm_index_free calls this: the executor state kept for the handle goes with it
+void exec_release(const void *index)
+{
+    std::lock_guard<std::mutex> lk(g_exec_mu);
+    g_exec.erase(index);
+}
+} // namespace drm
 
 // ------------------------------------------------------------------------------------ C ABI
 extern "C" {
@@ -280,7 +369,7 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
 {
     return guard([&] {
         search_rerank(index, refs, x, n, d, k_clusters, ef, queries, q_len, q_stride, stride, k, D, I, sw_scores,
-                      sw_ids, status, stats, 0);
+                      sw_ids, status, stats);
     });
 }
 
@@ -360,6 +449,30 @@ int drm_multi_create(const char *index_path, const int *devices, int ndev, const
     });
 }
 
+int drm_multi_create_genome(const char *index_path, const int *devices, int ndev, const uint8_t *genome, int64_t len,
+                            int32_t ref_len, drm_multi **out)
+{
+    return guard([&] {
+        if (!index_path || !devices || !out || ndev <= 0 || (!genome && len > 0))
+            throw Error(DRM_ERR_ARG, "null argument or no device");
+        *out = nullptr;
+        std::unique_ptr<drm_multi> m(new drm_multi());
+        m->devices.assign(devices, devices + ndev);
+        m->index.assign((size_t)ndev, nullptr);
+        m->refs.assign((size_t)ndev, nullptr);
+        try {
+            fan_out(ndev, [&](int r) {
+                abi_check(drm_index_load(index_path, m->devices[(size_t)r], &m->index[(size_t)r]));
+                abi_check(drm_refs_create_genome(genome, len, ref_len, m->devices[(size_t)r], &m->refs[(size_t)r]));
+            });
+        } catch (...) {
+            free_multi(m.get());
+            throw;
+        }
+        *out = m.release();
+    });
+}
+
 int drm_multi_free(drm_multi *m)
 {
     return guard([&] {
@@ -402,7 +515,7 @@ int drm_multi_search_rerank(drm_multi *m, const float *x, int64_t n, int32_t d, 
                           k_clusters, ef, rr ? queries + (size_t)lo * q_stride : nullptr, rr ? q_len + lo : nullptr,
                           q_stride, stride, k, D + (size_t)lo * kc, I + (size_t)lo * kc,
                           rr ? sw_scores + (size_t)lo * kr : nullptr, rr ? sw_ids + (size_t)lo * kr : nullptr,
-                          rr ? status + lo : nullptr, &st[(size_t)r], 0);
+                          rr ? status + lo : nullptr, &st[(size_t)r]);
         });
         if (stats) {
             *stats = drm_search_stats{};

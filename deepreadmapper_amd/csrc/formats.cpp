@@ -310,3 +310,88 @@ void read_file(const std::string &path, std::vector<std::string> &seqs, std::vec
 }
 
 } // namespace drm
+
+// ----------------------------------------------------------------------- extract_FASTA_sequence
+std::string drm::extract_fasta_sequence(const std::string &path)
+{
+    const std::string data = read_whole_file(path);
+    size_t p = data.find('\n');
+    p = p == std::string::npos ? data.size() : p + 1; // skip the first (header) line
+    std::string g;
+    g.reserve(data.size() - p);
+    for (; p < data.size(); ++p) {
+        const unsigned char c = (unsigned char)data[p];
+        if (std::isspace(c))
+            continue;
+        const char u = (char)std::toupper(c);
+        if (u == 'A' || u == 'T' || u == 'C' || u == 'G' || u == 'N')
+            g.push_back(u);
+    }
+    return g;
+}
+
+// ----------------------------------------------------------------------- SAM (write_sam)
+void drm::write_sam_block(const std::string &path, bool header, const std::string &ref_name, size_t ref_len,
+                          const std::vector<std::string> &query_seqs, const std::vector<std::string> &query_ids,
+                          size_t q0, size_t nq, const uint64_t *ids, const int32_t *counts, size_t k)
+{
+    std::ofstream out(path, header ? std::ios::out : std::ios::app);
+    if (!out.is_open())
+        throw Error(DRM_ERR_IO, "Failed to open SAM file: " + path);
+    if (header) {
+        out << "@HD\tVN:1.0\tSO:unsorted\n";
+        out << "@SQ\tSN:" << ref_name << "\tLN:" << ref_len << "\n";
+    }
+    std::string buf;
+    for (size_t i = 0; i < nq; ++i) {
+        const size_t g = q0 + i;
+        std::string clean = query_seqs[g]; // PREFIX "<" / POSTFIX ">" stripped (parse_inputs.hpp:10-11)
+        if (clean.size() > 2)
+            clean = clean.substr(1, clean.size() - 2);
+        const std::string qname = (g < query_ids.size() && !query_ids[g].empty()) ? query_ids[g]
+                                                                                  : "S1/" + std::to_string(g + 1) + "/0";
+        const std::string cigar = std::to_string(clean.size()) + "M";
+        for (int j = 0; j < counts[i] && (size_t)j < k; ++j) {
+            const uint64_t sid = ids[i * k + (size_t)j];
+            int flag = j == 0 ? 0 : 256; // primary / secondary
+            if (sid % 2 == 1)
+                flag |= 16; // reverse complement
+            buf += qname;
+            buf += '\t';
+            buf += std::to_string(flag);
+            buf += '\t';
+            buf += ref_name;
+            buf += '\t';
+            buf += std::to_string(sid / 2 + 1); // 1-based position
+            buf += "\t60\t";
+            buf += cigar;
+            buf += "\t*\t0\t0\t";
+            buf += clean;
+            buf += "\t*\n";
+        }
+        if (buf.size() > (1u << 22)) {
+            out << buf;
+            buf.clear();
+        }
+    }
+    out << buf;
+}
+
+extern "C" int drm_extract_fasta_sequence(const char *path, uint8_t *out, int64_t *len)
+{
+    try {
+        if (!path || !len)
+            throw drm::Error(DRM_ERR_ARG, "null argument");
+        const std::string g = drm::extract_fasta_sequence(path);
+        if (out)
+            std::memcpy(out, g.data(), std::min<size_t>(g.size(), (size_t)std::max<int64_t>(*len, 0)));
+        *len = (int64_t)g.size();
+        return DRM_OK;
+    } catch (const drm::Error &e) {
+        drm::set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception &e) {
+        drm::set_last_error(e.what());
+        return DRM_ERR_IO;
+    }
+}

@@ -1010,6 +1010,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
 
 } // namespace
 
+// Per-slot search workspace (visited bitmaps, clear lists, queue counters, the lean kernel's push log)
+// for a full-occupancy grid, allocated once at index load so that no search pays for it (at C5 the
+// bitmaps alone are 32 GB). Searches that need more (other LUT sizes, larger logs) still grow it.
+void reserve_search_scratch(DeviceIndex &ix)
+{
+    int cus = 0;
+    DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
+    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub;
+    if (lds == 0 || lds > 160 * 1024)
+        return;
+    const int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
+    const int slots = cus * per_cu;
+    ix.vis_words = std::max<int64_t>((ix.ntotal + 31) / 32, 1);
+    ix.clear_cap = 16384;
+    DRM_HIP_CHECK(hipMalloc(&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
+    DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
+    DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)slots * (size_t)ix.clear_cap));
+    ix.n_slots = slots;
+    DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
+    const int cap = std::max(ix.log_cap_req, 128 + 64); // what the lean kernel asks for at ef = 128
+    DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)slots * (size_t)cap));
+    ix.log_cap = cap;
+    ix.log_slots = slots;
+}
+
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream)
 {

@@ -26,6 +26,73 @@ namespace drm {
 namespace {
 
 constexpr int kPadRow = 256; // profile row index for "matches nothing"
+constexpr uint32_t kNoWindow = 0xFFFFFFFFu; // dynamic lookup: an id whose window lies outside the genome
+
+// comp_table of the reference (src/utils/parse_inputs.cpp:5-14): A<->T, C<->G, N->N, anything else 0
+__device__ __forceinline__ int comp_byte(int c)
+{
+    return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'N' ? 'N' : 0;
+}
+
+// Bytes of one candidate window: the static table row, or (dynamic lookup, find_sequence
+// src/utils/post_processor.cpp:47-64) genome[w / 2 ..+ ref_len), reverse-complemented for odd w;
+// a window past the genome end is the empty string (every row reads as the pad byte -1).
+struct CandRow {
+    const uint8_t *p;
+    int rc;
+    __device__ __forceinline__ CandRow(const RerankArgs &a, uint64_t w)
+    {
+        if (a.genome) {
+            const uint64_t pos = w >> 1;
+            const bool ok = w != (uint64_t)kNoWindow && pos + (uint64_t)a.ref_len <= (uint64_t)a.glen;
+            rc = (int)(w & 1u);
+            p = ok ? a.genome + pos + (rc ? a.ref_len - 1 : 0) : nullptr;
+        } else {
+            p = a.refs + w * (uint64_t)a.row_stride;
+            rc = 0;
+        }
+    }
+    __device__ __forceinline__ int at(int i) const
+    {
+        if (!p)
+            return -1;
+        return rc ? comp_byte(p[-i]) : (int)p[i];
+    }
+};
+
+// find_sequences' candidate list of query q into cand[] (one thread); returns the count, -2 past
+// kMaxCands. Static (:204-336): dense ids >= n_ref are dropped; sparse expansions are clipped to n_ref.
+// Dynamic (:72-201): dense keeps every id (out-of-genome windows are empty); the sparse expansion is
+// checked against the genome length. Duplicates are kept (the mapping restores the original count).
+template <typename T>
+__device__ int find_candidates(const RerankArgs &a, const int64_t *nb, int nsel, T *cand)
+{
+    const uint64_t limit = a.genome ? (uint64_t)a.glen : (uint64_t)a.n_ref;
+    int nc = 0;
+    for (int i = 0; i < nsel; ++i) {
+        const uint64_t id = (uint64_t)nb[i];
+        if (a.stride == 1) {
+            if (a.genome || id < limit) {
+                if (nc >= kMaxCands)
+                    return -2;
+                cand[nc++] = a.genome ? (T)(id < (uint64_t)kNoWindow ? id : kNoWindow) : (T)id;
+            }
+            continue;
+        }
+        const uint64_t s = (uint64_t)a.stride;
+        const uint64_t actual = id * s;
+        if (actual >= limit)
+            continue;
+        const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
+        const uint64_t end = min(actual + s, limit);
+        for (uint64_t pos = start; pos < end; ++pos) {
+            if (nc >= kMaxCands)
+                return -2;
+            cand[nc++] = (T)pos;
+        }
+    }
+    return nc;
+}
 
 // One DP row update for the full register row H[0..LQ).
 template <int LQ>
@@ -213,7 +280,7 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
         const int qlen = a.q_len[q];
         const int nsel = min(a.k_clusters, a.kk);
         const int64_t *nb = a.neighbors + q * a.kk;
-        if (a.stride == 1 && nsel <= kMaxCands) {
+        if (a.stride == 1 && nsel <= kMaxCands && !a.genome) {
             // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
             int base = 0;
             for (int c = 0; c < nsel; c += 64) {
@@ -228,35 +295,7 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
             if (tid == 0)
                 ncand_s = base;
         } else if (tid == 0) {
-            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride), duplicates kept
-            int nc = 0;
-            bool overflow = false;
-            for (int i = 0; i < nsel && !overflow; ++i) {
-                const uint64_t id = (uint64_t)nb[i];
-                if (a.stride == 1) {
-                    if (id < (uint64_t)a.n_ref) {
-                        if (nc >= kMaxCands)
-                            overflow = true;
-                        else
-                            cand[nc++] = id;
-                    }
-                    continue;
-                }
-                const uint64_t s = (uint64_t)a.stride;
-                const uint64_t actual = id * s;
-                if (actual >= (uint64_t)a.n_ref)
-                    continue;
-                const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
-                const uint64_t end = min(actual + s, (uint64_t)a.n_ref);
-                for (uint64_t pos = start; pos < end; ++pos) {
-                    if (nc >= kMaxCands) {
-                        overflow = true;
-                        break;
-                    }
-                    cand[nc++] = pos;
-                }
-            }
-            ncand_s = overflow ? -2 : nc;
+            ncand_s = find_candidates(a, nb, nsel, cand);
         }
         for (int t = tid; t < LQ; t += blockDim.x)
             qbuf[t] = (t < qlen) ? a.queries[q * a.q_stride + t] : 0;
@@ -276,25 +315,27 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
                 H[j] = 0u;
             us2 best = {0, 0};
             const uint64_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
-            const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
-            const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
+            const CandRow ra(a, wa), rb(a, wb);
             const int L = a.ref_len;
-            int na = (L > 0) ? (int)pa[0] : kPadRow;
-            int nb2 = (L > 0 && has_b) ? (int)pb[0] : kPadRow;
+            auto code = [](int c) { return c < 0 ? kPadRow : c; };
+            int na = (L > 0) ? code(ra.at(0)) : kPadRow;
+            int nb2 = (L > 0 && has_b) ? code(rb.at(0)) : kPadRow;
             for (int i = 0; i < L; ++i) {
                 const int ca = na, cb = nb2;
                 if (i + 1 < L) { // prefetch the next row's bytes
-                    na = pa[i + 1];
-                    nb2 = has_b ? (int)pb[i + 1] : kPadRow;
+                    na = code(ra.at(i + 1));
+                    nb2 = has_b ? code(rb.at(i + 1)) : kPadRow;
                 }
                 uint32_t pw[(LQ + 7) / 8];
                 load_profile_pk<LQ>(prof, ca, cb, pw);
                 sw_row_pk<LQ>(H, pw, best);
             }
-            a.cand_ids[q * a.cmax + c0] = wa;
+            // dense dynamic lookup reports the search's own id (e.g. -1 as 2^64-1, post_processor.cpp:95-101)
+            const bool dense_dyn = a.genome && a.stride == 1;
+            a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
             a.cand_scores[q * a.cmax + c0] = (int32_t)best.x;
             if (has_b) {
-                a.cand_ids[q * a.cmax + c1] = wb;
+                a.cand_ids[q * a.cmax + c1] = dense_dyn ? (uint64_t)nb[c1] : wb;
                 a.cand_scores[q * a.cmax + c1] = (int32_t)best.y;
             }
         }
@@ -386,7 +427,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         const int qlen = a.q_len[q];
         const int nsel = min(a.k_clusters, a.kk);
         const int64_t *nb = a.neighbors + q * a.kk;
-        if (a.stride == 1 && nsel <= kMaxCands) {
+        if (a.stride == 1 && nsel <= kMaxCands && !a.genome) {
             // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
             int base = 0;
             for (int c = 0; c < nsel; c += 64) {
@@ -401,36 +442,8 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             if (tid == 0)
                 ncand_s = base;
         } else if (tid == 0) {
-            // sparse (:238-335): expand sparse_id*stride to [pos-stride+1, pos+stride); the expansion
-            // is mapped back to the original count (:502-507), so duplicates are kept
-            int nc = 0;
-            bool overflow = false;
-            for (int i = 0; i < nsel && !overflow; ++i) {
-                const uint64_t id = (uint64_t)nb[i];
-                if (a.stride == 1) {
-                    if (id < (uint64_t)a.n_ref) {
-                        if (nc >= kMaxCands)
-                            overflow = true;
-                        else
-                            cand[nc++] = (uint32_t)id;
-                    }
-                    continue;
-                }
-                const uint64_t s = (uint64_t)a.stride;
-                const uint64_t actual = id * s;
-                if (actual >= (uint64_t)a.n_ref)
-                    continue;
-                const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
-                const uint64_t end = min(actual + s, (uint64_t)a.n_ref);
-                for (uint64_t pos = start; pos < end; ++pos) {
-                    if (nc >= kMaxCands) {
-                        overflow = true;
-                        break;
-                    }
-                    cand[nc++] = (uint32_t)pos;
-                }
-            }
-            ncand_s = overflow ? -2 : nc;
+            // sparse (:238-335) or dynamic lookup: expand, duplicates kept (:502-507)
+            ncand_s = find_candidates(a, nb, nsel, cand);
         }
         for (int t = tid; t < ((LQ + 15) & ~15); t += 64)
             qbuf[t] = (t < qlen && t < LQ) ? a.queries[q * a.q_stride + t] : 0;
@@ -465,6 +478,23 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
             // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
             // block in flight while the current one is consumed), not one byte load per row
+            if (a.genome) { // dynamic lookup: unaligned windows, one byte per row (genome bytes are ACGTN)
+                const CandRow ra(a, wa), rb(a, wb);
+                const int L = a.ref_len;
+                for (int i = 0; i < L; ++i) {
+                    const int ca = ra.at(i), cb = has_b ? rb.at(i) : -1;
+                    int ka = acgt_code(ca), kb = acgt_code(cb);
+                    if (ka < 0) { // N (or the empty window, -1): "a byte the query lacks" unless it has it
+                        flagged |= ca >= 0 && ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
+                        ka = 4;
+                    }
+                    if (kb < 0) {
+                        flagged |= cb >= 0 && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
+                        kb = 4;
+                    }
+                    sw_row_f16<LQ>(H, pprof + ka * GST + kb * PST, best);
+                }
+            } else {
 #if DRM_SW_BLOCKLOAD
             const uint4 *pa = reinterpret_cast<const uint4 *>(a.refs + (size_t)wa * (size_t)a.row_stride);
             const uint4 *pb = reinterpret_cast<const uint4 *>(a.refs + (size_t)wb * (size_t)a.row_stride);
@@ -519,10 +549,12 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 }
                 sw_row_f16<LQ>(H, pprof + ka * GST + kb * PST, best);
             }
-            a.cand_ids[q * a.cmax + c0] = wa;
+            }
+            const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
+            a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
             a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);
             if (has_b) {
-                a.cand_ids[q * a.cmax + c1] = wb;
+                a.cand_ids[q * a.cmax + c1] = dense_dyn ? (uint64_t)nb[c1] : wb;
                 a.cand_scores[q * a.cmax + c1] = (int32_t)((float)best.y * 1024.0f);
             }
         }

@@ -53,10 +53,15 @@ def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None,
 class MultiIndex:
     """drm_multi: one IndexHNSWPQ replica (+ window table) per entry of `devices` (repeats allowed)."""
 
-    def __init__(self, path, devices, windows=None):
+    def __init__(self, path, devices, windows=None, genome=None, ref_len=150):
         devs = np.ascontiguousarray(devices, dtype=np.int32)
         h = C.c_void_p()
-        if windows is not None:
+        if genome is not None:  # dynamic lookup (use_dynamic)
+            g = np.frombuffer(genome, dtype=np.uint8) if isinstance(genome, (bytes, bytearray)) else \
+                np.ascontiguousarray(genome, dtype=np.uint8)
+            check(lib().drm_multi_create_genome(str(path).encode(), ptr(devs), len(devs), ptr(g), g.size, int(ref_len),
+                                                C.byref(h)))
+        elif windows is not None:
             w = np.ascontiguousarray(windows, dtype=np.uint8)
             check(lib().drm_multi_create(str(path).encode(), ptr(devs), len(devs), ptr(w), w.shape[0], w.shape[1],
                                          w.shape[1], C.byref(h)))
@@ -64,7 +69,7 @@ class MultiIndex:
             check(lib().drm_multi_create(str(path).encode(), ptr(devs), len(devs), None, 0, 0, 0, C.byref(h)))
         self._h = h.value
         self.devices = list(devs)
-        self.has_refs = windows is not None
+        self.has_refs = windows is not None or genome is not None
         info = IndexInfo()
         check(lib().drm_multi_get_index_info(self._h, C.byref(info)))
         self.info = info

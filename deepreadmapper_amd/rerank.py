@@ -71,6 +71,91 @@ class WindowTable:
             pass
 
 
+class GenomeTable:
+    """Device-resident genome string for the dynamic lookup (use_dynamic): window id w is
+    genome[w // 2 : w // 2 + ref_len], reverse-complemented when w is odd (find_sequence,
+    src/utils/post_processor.cpp:47-64)."""
+
+    def __init__(self, genome, ref_len, device=0):
+        g = np.frombuffer(genome, dtype=np.uint8) if isinstance(genome, (bytes, bytearray)) else \
+            np.ascontiguousarray(genome, dtype=np.uint8)
+        self.glen, self.ref_len = int(g.size), int(ref_len)
+        h = C.c_void_p()
+        check(lib().drm_refs_create_genome(ptr(g) if g.size else None, g.size, int(ref_len), int(device), C.byref(h)))
+        self._h = h.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def free(self):
+        if self._h:
+            check(lib().drm_refs_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                self.free()
+        except Exception:
+            pass
+
+
+def extract_fasta_sequence(path):
+    """extract_FASTA_sequence (src/utils/parse_inputs.cpp:174-220) -> bytes."""
+    n = C.c_int64(0)
+    check(lib().drm_extract_fasta_sequence(str(path).encode(), None, C.byref(n)))
+    out = np.empty(max(n.value, 1), dtype=np.uint8)
+    n2 = C.c_int64(n.value)
+    check(lib().drm_extract_fasta_sequence(str(path).encode(), ptr(out), C.byref(n2)))
+    return bytes(out[:n.value])
+
+
+def rerank_dynamic_arrays(genome_table, neighbors, query_seqs, stride, k, k_clusters):
+    """Array form of post_process_sw_dynamic on a GenomeTable: (scores, ids, counts) like rerank_arrays."""
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    nq, kk = nb.shape
+    qbuf, qlen = query_seqs if isinstance(query_seqs, tuple) else pack_queries(query_seqs)
+    scores = np.empty((nq, k), dtype=np.int32)
+    ids = np.empty((nq, k), dtype=np.uint64)
+    counts = np.empty(nq, dtype=np.int32)
+    bad = C.c_int64(-1)
+    check(lib().drm_post_process_sw_dynamic(genome_table.handle, ptr(nb), nq, kk, ptr(qbuf), ptr(qlen), qbuf.shape[1],
+                                            int(stride), int(k), int(k_clusters), ptr(scores), ptr(ids), ptr(counts),
+                                            C.byref(bad)))
+    return scores, ids, counts
+
+
+def post_process_sw_dynamic(neighbors, distances, ref_genome, query_seqs, ref_len, stride, k, k_clusters):
+    """post_process_sw_dynamic (src/utils/post_processor.cpp:357-452): flattened (final_seqs,
+    final_scores, final_ids); ref_genome is the genome string (bytes / str) or a GenomeTable."""
+    g = ref_genome.encode() if isinstance(ref_genome, str) else ref_genome
+    table = g if isinstance(g, GenomeTable) else GenomeTable(g, ref_len)
+    nb = np.asarray([list(r) for r in neighbors], dtype=np.int64) if not isinstance(neighbors, np.ndarray) else neighbors
+    try:
+        scores, ids, counts = rerank_dynamic_arrays(table, nb, query_seqs, stride, k, k_clusters)
+    except DrmError as e:
+        raise RuntimeError(str(e)) from e
+    seqs, sc, fid = [], [], []
+    for i in range(len(counts)):
+        for j in range(int(counts[i])):
+            wid = int(ids[i, j])
+            sc.append(int(scores[i, j]))
+            fid.append(wid)
+            if not isinstance(g, GenomeTable):
+                pos = wid // 2
+                w = g[pos:pos + ref_len] if pos + ref_len <= len(g) else b""
+                if wid % 2 == 1 and w:
+                    w = bytes(_COMP_TABLE[np.frombuffer(w, dtype=np.uint8)[::-1]])
+                seqs.append(bytes(w))
+    return seqs, sc, fid
+
+
+_COMP_TABLE = np.zeros(256, dtype=np.uint8)
+for _a, _b in zip(b"ATCGN", b"TAGCN"):
+    _COMP_TABLE[_a] = _b
+
+
 def pack_queries(query_seqs):
     qs = [_as_bytes(q) for q in query_seqs]
     stride = max([len(q) for q in qs] + [1])

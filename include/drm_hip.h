@@ -156,6 +156,17 @@ int drm_sw_scores(const uint8_t *s1, const int64_t *off1, const int32_t *len1, c
 int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int64_t row_stride, int device,
                     drm_refs **out);
 int drm_refs_free(drm_refs *refs);
+/* Dynamic lookup (pipeline's use_dynamic, src/main.cpp:182-185): the genome string itself
+ * (extract_FASTA_sequence, src/utils/parse_inputs.cpp:174-220 -- drm_extract_fasta_sequence) on the
+ * device instead of the 2*(L - ref_len + 1)-window table: window id w is genome[w/2 ..+ ref_len),
+ * reverse-complemented (comp_table) when w is odd (find_sequence, src/utils/post_processor.cpp:47-64).
+ * Genomes of up to 2^31 - 1 bases. */
+int drm_refs_create_genome(const uint8_t *genome, int64_t len, int32_t ref_len, int device, drm_refs **out);
+int drm_refs_is_genome(const drm_refs *refs, int *is_genome);
+/* extract_FASTA_sequence: the file's first line is skipped, whitespace dropped, letters upper-cased
+ * and only A/C/G/T/N kept (from every later line, headers included -- the reference's behaviour).
+ * Two calls: *len receives the length (out may be NULL), then out[0 .. *len) the sequence. */
+int drm_extract_fasta_sequence(const char *path, uint8_t *out, int64_t *len);
 /* Shape and device of a window table (any out-pointer may be NULL). */
 int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device);
 
@@ -194,7 +205,8 @@ int drm_host_free(void *ptr);
  * consecutive batches overlap on three streams; batch size DRM_BATCH, default 262144 queries).
  * Host pointers throughout:
  *   x [n x d] f32 -> D [n x k_clusters] f32, I [n x k_clusters] int64 (drm_search's outputs);
- *   refs == NULL: search only (queries ... status ignored);
+ *   refs == NULL: search only (queries ... status ignored); a genome handle (drm_refs_create_genome)
+ *   reranks with the dynamic lookup (post_process_sw_dynamic), a window table with the static one;
  *   else queries [n x q_stride] bytes with q_len[n] -> sw_scores / sw_ids [n x k] and status[n]
  *   (drm_post_process_sw_static_device's per-query status: k or 0 rows emitted, -1 not enough
  *   candidates, -2 / -3 candidate or length limits).
@@ -216,6 +228,9 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
 typedef struct drm_multi drm_multi;
 int drm_multi_create(const char *index_path, const int *devices, int ndev, const uint8_t *windows, int64_t n_ref,
                      int32_t ref_len, int64_t row_stride, drm_multi **out);
+/* The same with the dynamic lookup: a genome handle per device (drm_refs_create_genome). */
+int drm_multi_create_genome(const char *index_path, const int *devices, int ndev, const uint8_t *genome, int64_t len,
+                            int32_t ref_len, drm_multi **out);
 int drm_multi_free(drm_multi *m);
 int drm_multi_get_index_info(const drm_multi *m, drm_index_info *info); /* replica 0's info */
 int drm_multi_search_rerank(drm_multi *m, const float *x, int64_t n, int32_t d, int32_t k_clusters, int32_t ef,
@@ -236,6 +251,19 @@ int drm_comm_init(const uint8_t *id, int nranks, int rank, int device, drm_comm 
 int drm_comm_free(drm_comm *comm);
 int drm_comm_gather_rows(drm_comm *comm, const void *d_send, int64_t n_total, int64_t row_bytes, void *d_recv, int root,
                          void *stream);
+
+/* post_process_sw_dynamic (src/utils/post_processor.cpp:357-452) on a genome handle: the same
+ * contract as drm_post_process_sw_static, with find_sequences' dynamic candidate rules (dense: every
+ * one of the first min(k_clusters, kk) ids, an out-of-genome window scoring 0 and keeping its id;
+ * sparse: the expansion checked against the genome length). */
+int drm_post_process_sw_dynamic(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                                const uint8_t *queries, const int32_t *q_len, int32_t q_stride, int64_t stride,
+                                int32_t k, int32_t k_clusters, int32_t *top_scores, uint64_t *top_ids,
+                                int32_t *counts, int64_t *bad_query);
+int drm_post_process_sw_dynamic_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                       const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                                       int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
+                                       uint64_t *d_top_ids, int32_t *d_status, void *stream);
 
 /* ---------------------------------------------------------------- index build (hnswpq_index)
  * build_faiss_index (src/hnswpq/index.cpp:86-193): trains PQ on an evenly spaced sample of

@@ -226,6 +226,130 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
 }
 
 /* ========================================================================================
+ * post_process_sw_dynamic (src/utils/post_processor.cpp:357-452): candidate windows cut from the
+ * genome string (extract_FASTA_sequence, src/utils/parse_inputs.cpp:174-220) by find_sequences
+ * dynamic (:72-201) / find_sequence (:47-64), then sw_reranker.
+ *   dense (stride 1): every one of the first min(k_clusters, n) ids is a candidate (no range check;
+ *     an id whose window runs past the genome -- e.g. -1 -> 2^64-1 -- is the empty string, score 0);
+ *   sparse: actual = id * stride is checked against the GENOME LENGTH and the expansion
+ *     [actual - stride + 1, actual + stride) is clipped to it (the reference's quirk), duplicates kept.
+ * find_sequence: window id -> position id / 2, reverse complement (comp_table :5-14) when id is odd.
+ * ====================================================================================== */
+static uint8_t comp_byte(uint8_t c)
+{
+    switch (c) {
+    case 'A': return 'T';
+    case 'T': return 'A';
+    case 'C': return 'G';
+    case 'G': return 'C';
+    case 'N': return 'N';
+    default: return 0;
+    }
+}
+
+/* find_sequence: the window of dense id `id` into buf (ref_len bytes), returns its length (0 = "") */
+static int64_t find_sequence_dyn(const uint8_t *g, int64_t glen, uint64_t id, int64_t ref_len, uint8_t *buf)
+{
+    const uint64_t pos = id / 2;
+    if (pos + (uint64_t)ref_len > (uint64_t)glen)
+        return 0;
+    if (id % 2 == 1)
+        for (int64_t i = 0; i < ref_len; ++i)
+            buf[i] = comp_byte(g[pos + (uint64_t)(ref_len - 1 - i)]);
+    else
+        memcpy(buf, g + pos, (size_t)ref_len);
+    return ref_len;
+}
+
+static int64_t ppd_one_query(const int64_t *nb, int64_t kk, const uint8_t *g, int64_t glen, int64_t ref_len,
+                             const uint8_t *q, int32_t qlen, int64_t stride, int64_t k, int64_t k_clusters,
+                             int32_t *out_scores, uint64_t *out_ids)
+{
+    const int64_t nsel = k_clusters < kk ? k_clusters : kk;
+    int64_t cap = (stride == 1) ? (nsel > 0 ? nsel : 1) : (nsel * (2 * stride) + 1);
+    uint64_t *cand = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)cap);
+    int64_t ncand = 0;
+    if (stride == 1) {
+        for (int64_t i = 0; i < nsel; ++i)
+            cand[ncand++] = (uint64_t)nb[i];
+    } else {
+        for (int64_t i = 0; i < nsel; ++i) {
+            uint64_t actual = (uint64_t)nb[i] * (uint64_t)stride;
+            if (actual >= (uint64_t)glen)
+                continue;
+            uint64_t start = (actual >= (uint64_t)(stride - 1)) ? actual - (uint64_t)stride + 1 : 0;
+            uint64_t end = actual + (uint64_t)stride;
+            if (end > (uint64_t)glen)
+                end = (uint64_t)glen;
+            for (uint64_t pos = start; pos < end; ++pos)
+                cand[ncand++] = pos;
+        }
+    }
+    if (ncand == 0 || k == 0) {
+        free(cand);
+        return 0;
+    }
+    int32_t *scores = (int32_t *)malloc(sizeof(int32_t) * (size_t)ncand);
+    uint8_t *buf = (uint8_t *)malloc((size_t)(ref_len > 0 ? ref_len : 1));
+    for (int64_t c = 0; c < ncand; ++c) {
+        const int64_t len = find_sequence_dyn(g, glen, cand[c], ref_len, buf);
+        scores[c] = oracle_calc_sw_score(buf, len, q, qlen);
+    }
+    free(buf);
+    if (ncand < k) {
+        free(scores);
+        free(cand);
+        return -1;
+    }
+    int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)ncand);
+    for (int64_t c = 0; c < ncand; ++c)
+        idx[c] = c;
+    oracle_partial_sort_desc(idx, ncand, k, scores);
+    for (int64_t j = 0; j < k; ++j) {
+        out_scores[j] = scores[idx[j]];
+        out_ids[j] = cand[idx[j]];
+    }
+    free(idx);
+    free(scores);
+    free(cand);
+    return k;
+}
+
+int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *genome,
+                                       int64_t glen, int64_t ref_len, const uint8_t *queries, const int32_t *q_len,
+                                       int64_t q_stride, int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
+                                       int32_t *top_scores, uint64_t *top_ids, int32_t *counts)
+{
+    if (k > k_clusters * 2 * stride) /* :390-393 */
+        return -1000000000;
+    int64_t first_bad = -1;
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic)
+#endif
+    for (int64_t i = 0; i < nq; ++i) {
+        for (int64_t j = 0; j < k; ++j) {
+            top_scores[i * k + j] = -1;
+            top_ids[i * k + j] = UINT64_MAX;
+        }
+        int64_t r = ppd_one_query(neighbors + i * kk, kk, genome, glen, ref_len, queries + i * q_stride, q_len[i],
+                                  stride, k, k_clusters, top_scores + i * k, top_ids + i * k);
+        counts[i] = r < 0 ? 0 : (int32_t)r;
+        if (r < 0) {
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+            {
+                if (first_bad < 0 || i < first_bad)
+                    first_bad = i;
+            }
+        }
+    }
+    return first_bad >= 0 ? -(1 + first_bad) : 0;
+}
+
+/* ========================================================================================
  * faiss IndexHNSWPQ search [upstream faiss >= 1.8].
  * ====================================================================================== */
 

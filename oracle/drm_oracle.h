@@ -41,6 +41,11 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
                                       const uint8_t *queries, const int32_t *q_len, int64_t q_stride,
                                       int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
                                       int32_t *top_scores, uint64_t *top_ids, int32_t *counts);
+/* post_process_sw_dynamic (src/utils/post_processor.cpp:357-452) over the genome string */
+int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *genome,
+                                       int64_t glen, int64_t ref_len, const uint8_t *queries, const int32_t *q_len,
+                                       int64_t q_stride, int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
+                                       int32_t *top_scores, uint64_t *top_ids, int32_t *counts);
 
 /* ---- faiss IndexHNSWPQ (upstream semantics, see DESIGN.md "oracle") ---- */
 typedef struct {

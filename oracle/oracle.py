@@ -24,6 +24,7 @@ def lib():
         _lib.oracle_calc_sw_score.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
         _lib.oracle_partial_sort_desc.restype = None
         _lib.oracle_post_process_sw_static.restype = C.c_int64
+        _lib.oracle_post_process_sw_dynamic.restype = C.c_int64
         _lib.oracle_hnswpq_search.restype = C.c_int
         _lib.oracle_pq_distance_table.restype = None
     return _lib
@@ -86,6 +87,25 @@ def post_process_sw_static(neighbors, refs, ref_len, queries, q_len, stride, k, 
         _p(neighbors, C.c_int64), C.c_int64(nq), C.c_int64(kk),
         _p(refs, C.c_uint8), C.c_int64(refs.shape[0]), C.c_int64(ref_len), C.c_int64(refs.shape[1]),
         _p(queries, C.c_uint8), _p(q_len, C.c_int32), C.c_int64(queries.shape[1]),
+        C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int(nthreads),
+        _p(scores, C.c_int32), _p(ids, C.c_uint64), _p(counts, C.c_int32))
+    return int(rc), scores, ids, counts
+
+
+def post_process_sw_dynamic(neighbors, genome, ref_len, queries, q_len, stride, k, k_clusters, nthreads=0):
+    """post_process_sw_dynamic: neighbors [nq, kk] int64; genome uint8 (extract_FASTA_sequence);
+    queries [nq, q_stride] uint8."""
+    neighbors = np.ascontiguousarray(neighbors, dtype=np.int64)
+    genome = np.ascontiguousarray(genome, dtype=np.uint8)
+    queries = np.ascontiguousarray(queries, dtype=np.uint8)
+    q_len = np.ascontiguousarray(q_len, dtype=np.int32)
+    nq, kk = neighbors.shape
+    scores = np.zeros((nq, k), dtype=np.int32)
+    ids = np.zeros((nq, k), dtype=np.uint64)
+    counts = np.zeros(nq, dtype=np.int32)
+    rc = lib().oracle_post_process_sw_dynamic(
+        _p(neighbors, C.c_int64), C.c_int64(nq), C.c_int64(kk), _p(genome, C.c_uint8), C.c_int64(genome.size),
+        C.c_int64(ref_len), _p(queries, C.c_uint8), _p(q_len, C.c_int32), C.c_int64(queries.shape[1]),
         C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int(nthreads),
         _p(scores, C.c_int32), _p(ids, C.c_uint64), _p(counts, C.c_int32))
     return int(rc), scores, ids, counts

@@ -8,9 +8,13 @@
 // HNSW results exactly like save_results. The north-star tail (SW rerank, the commented-out
 // post_process_sw_static call at :333-341) runs on the GPU when query sequences are available and
 // adds sw_scores.npy (<i4) and sw_ids.npy (<u8) [n, k] (rows of a query with no candidate: -1 / 2^64-1).
+// use_dynamic cuts the candidate windows from the genome string on the device (post_process_sw_dynamic
+// instead of the static window table); use_streaming writes <output_dir>/results.sam block by block
+// (write_sam_streaming) and, like the reference, skips the .npy outputs -- the reference streams only in
+// its dynamic branch, so static + streaming writes no result file there either.
 // Differences, all documented in DESIGN.md: sequence inputs are embedded with the deterministic
-// 3-mer stand-in (the OpenVINO model is out of scope); use_dynamic / use_streaming (SAM streaming)
-// are not implemented (out of scope) and are rejected with an error instead of silently ignored.
+// 3-mer stand-in (the OpenVINO model is out of scope), and the rerank is the north star's SW rerank
+// (the reference's main runs an L2 rerank with the OpenVINO model at this point, src/main.cpp:312-331).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +22,7 @@
 #include <filesystem>
 #include <iostream>
 #include <numeric>
+#include <thread>
 
 #include "drm_hip.h"
 #include "drm_internal.h"
@@ -87,8 +92,7 @@ int main(int argc, char *argv[])
         const std::string out_dir = argc >= 8 ? argv[7] : ".";
         const bool use_dynamic = argc >= 9 && std::stoi(argv[8]) != 0;
         const bool use_streaming = argc >= 10 && std::stoi(argv[9]) != 0;
-        if (use_dynamic || use_streaming)
-            throw drm::Error(DRM_ERR_UNSUPPORTED, "use_dynamic / use_streaming are not supported by this build");
+        const std::string sam_file = out_dir + "/results.sam"; // src/main.cpp:67
         // devices: DRM_DEVICES=0,1,... fans the batch out over several GPUs (contiguous query shards,
         // replicated index); DRM_DEVICE=i picks one (default 0)
         std::vector<int> devices;
@@ -132,8 +136,17 @@ int main(int argc, char *argv[])
             }
             nq = qseqs.size();
         }
+        // ---- reference: the static window table (read_file(ref, ref_len, 1, lookup)), or with use_dynamic the
+        //      genome string (extract_FASTA_sequence), windows cut on the device (src/main.cpp:182-192)
+        const bool dyn = use_dynamic && !is_npy;
         std::vector<std::string> refs;
-        if (!is_npy) {
+        std::string genome;
+        if (dyn) {
+            std::cout << "[MAIN] Using DYNAMIC fetching for reference sequences" << std::endl;
+            genome = drm::extract_fasta_sequence(ref_file);
+            std::cout << "[MAIN] Loaded a " << genome.size() << " bp genome from " << ref_file << std::endl;
+        } else if (!is_npy) {
+            std::cout << "[MAIN] Using STATIC fetching for reference sequences" << std::endl;
             std::vector<std::string> dummy;
             drm::read_file(ref_file, refs, dummy, ref_len, 1, true);
             std::cout << "[MAIN] Loaded " << refs.size() << " reference sequences from " << ref_file << std::endl;
@@ -151,7 +164,7 @@ int main(int argc, char *argv[])
 
         // ---- window table (static ref_seqs) as one fixed-width block
         std::string table;
-        if (!is_npy) {
+        if (!is_npy && !dyn) {
             table.assign(refs.size() * ref_len, '\0');
             for (size_t r = 0; r < refs.size(); ++r)
                 std::memcpy(&table[r * ref_len], refs[r].data(), ref_len);
@@ -168,13 +181,21 @@ int main(int argc, char *argv[])
         if (devices.size() == 1) {
             check(drm_index_load(index_file.c_str(), device, &index));
             check(drm_index_get_info(index, &info));
-            if (!is_npy)
+            if (dyn)
+                check(drm_refs_create_genome((const uint8_t *)genome.data(), (int64_t)genome.size(), (int32_t)ref_len,
+                                             device, &rt));
+            else if (!is_npy)
                 check(drm_refs_create((const uint8_t *)table.data(), (int64_t)refs.size(), (int32_t)ref_len,
                                       (int64_t)ref_len, device, &rt));
         } else {
-            check(drm_multi_create(index_file.c_str(), devices.data(), (int)devices.size(),
-                                   is_npy ? nullptr : (const uint8_t *)table.data(), (int64_t)refs.size(),
-                                   (int32_t)ref_len, (int64_t)ref_len, &multi));
+            if (dyn)
+                check(drm_multi_create_genome(index_file.c_str(), devices.data(), (int)devices.size(),
+                                              (const uint8_t *)genome.data(), (int64_t)genome.size(), (int32_t)ref_len,
+                                              &multi));
+            else
+                check(drm_multi_create(index_file.c_str(), devices.data(), (int)devices.size(),
+                                       is_npy ? nullptr : (const uint8_t *)table.data(), (int64_t)refs.size(),
+                                       (int32_t)ref_len, (int64_t)ref_len, &multi));
             check(drm_multi_get_index_info(multi, &info));
         }
         std::cout << "[MAIN] Index loaded time: " << ms_since(t0) << " ms (" << info.ntotal << " vectors, "
@@ -220,14 +241,61 @@ int main(int argc, char *argv[])
         Pinned<uint64_t> sw_ids(is_npy ? 0 : nq * (size_t)k);
         t0 = clk::now();
         drm_search_stats st{};
-        int rc;
-        if (multi)
-            rc = drm_multi_search_rerank(multi, x.p, (int64_t)nq, (int32_t)dim, k_clusters, ef, is_npy ? nullptr : qbuf.p,
-                                         ql.p, (int32_t)qs, (int64_t)stride, k, D.p, I.p, sw_scores.p, sw_ids.p, status.p,
-                                         &st);
-        else
-            rc = drm_search_rerank(index, rt, x.p, (int64_t)nq, (int32_t)dim, k_clusters, ef, is_npy ? nullptr : qbuf.p,
-                                   ql.p, (int32_t)qs, (int64_t)stride, k, D.p, I.p, sw_scores.p, sw_ids.p, status.p, &st);
+        // one pass over queries [lo, lo + m) into the output arrays at row lo
+        auto run = [&](size_t lo, size_t m, drm_search_stats *sp) {
+            const uint8_t *qb = is_npy ? nullptr : qbuf.p + lo * qs;
+            if (multi)
+                return drm_multi_search_rerank(multi, x.p + lo * dim, (int64_t)m, (int32_t)dim, k_clusters, ef, qb,
+                                               ql.p + lo, (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters,
+                                               I.p + lo * k_clusters, sw_scores.p + lo * k, sw_ids.p + lo * k,
+                                               status.p + lo, sp);
+            return drm_search_rerank(index, rt, x.p + lo * dim, (int64_t)m, (int32_t)dim, k_clusters, ef, qb, ql.p + lo,
+                                     (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters, I.p + lo * k_clusters,
+                                     sw_scores.p + lo * k, sw_ids.p + lo * k, status.p + lo, sp);
+        };
+        int rc = DRM_OK;
+        const bool stream_sam = use_streaming && dyn;
+        if (stream_sam) {
+            // post_process_*_dynamic_streaming + write_sam_streaming (src/main.cpp:316-319,
+            // src/utils/utils.cpp:409-503): the SAM lines of each block are written by a host thread while the
+            // GPU works on the next block (blocks of DRM_SAM_BLOCK queries; the file does not depend on it)
+            std::cout << "[MAIN] Using STREAMING output to SAM file: " << sam_file << std::endl;
+            std::filesystem::create_directories(out_dir);
+            size_t block = 1u << 20;
+            if (const char *e = std::getenv("DRM_SAM_BLOCK"))
+                block = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+            std::thread writer;
+            std::string werr;
+            for (size_t lo = 0; lo < nq && rc == DRM_OK; lo += block) {
+                const size_t m = std::min(block, nq - lo);
+                drm_search_stats bs{};
+                rc = run(lo, m, &bs);
+                st.nq += bs.nq;
+                st.ndis += bs.ndis;
+                st.nhops += bs.nhops;
+                st.kernel_ms += bs.kernel_ms;
+                if (writer.joinable())
+                    writer.join();
+                if (rc == DRM_OK && werr.empty())
+                    writer = std::thread([&, lo, m] {
+                        try {
+                            std::vector<int32_t> cnt(m);
+                            for (size_t i = 0; i < m; ++i)
+                                cnt[i] = std::max(status.p[lo + i], 0);
+                            drm::write_sam_block(sam_file, lo == 0, "ref", ref_len, qseqs, qids, lo, m,
+                                                 sw_ids.p + lo * k, cnt.data(), (size_t)k);
+                        } catch (const std::exception &e) {
+                            werr = e.what();
+                        }
+                    });
+            }
+            if (writer.joinable())
+                writer.join();
+            if (rc == DRM_OK && !werr.empty())
+                throw drm::Error(DRM_ERR_IO, werr);
+        } else {
+            rc = run(0, nq, &st);
+        }
         const std::string err = rc == DRM_OK ? "" : drm_last_error();
         if (rt)
             drm_refs_free(rt);
@@ -247,7 +315,13 @@ int main(int argc, char *argv[])
                     sw_ids.p[i * (size_t)k + (size_t)j] = ~0ull;
                 }
 
-        // ---- outputs (save_results, src/utils/utils.cpp:264-334)
+        // ---- outputs (save_results, src/utils/utils.cpp:264-334); skipped with use_streaming (src/main.cpp:371, :409-412)
+        if (use_streaming) {
+            std::cout << "[MAIN] Skip normal output saving since streaming output is used." << std::endl;
+            std::cout << "[MAIN] Total pipeline time: " << ms_since(master) << " ms" << std::endl;
+            std::cout << "=== Pipeline Completed Successfully! ===" << std::endl;
+            return 0;
+        }
         t0 = clk::now();
         std::filesystem::create_directories(out_dir);
         const size_t kout = stride == 1 ? (size_t)k : (size_t)k_clusters;
