@@ -32,9 +32,14 @@ def genome_case():
 
 def _both(table, g, nb, q, ql, stride, k, kc):
     from deepreadmapper_amd import rerank_dynamic_arrays
-    sc, ids, cnt = rerank_dynamic_arrays(table, nb, (q, ql), stride, k, kc)
+    from deepreadmapper_amd._native import DrmError, DRM_ERR_CANDS
     rc, sco, ido, cnto = O.post_process_sw_dynamic(nb, g, 150, q, ql, stride, k, kc)
-    assert rc == 0
+    if rc < 0:  # some query has 0 < candidates < k: sw_reranker throws (reranker.cpp:26-29), so does the GPU
+        with pytest.raises(DrmError) as e:
+            rerank_dynamic_arrays(table, nb, (q, ql), stride, k, kc)
+        assert e.value.code == DRM_ERR_CANDS
+        return None, None
+    sc, ids, cnt = rerank_dynamic_arrays(table, nb, (q, ql), stride, k, kc)
     assert np.array_equal(cnt, cnto) and np.array_equal(sc, sco) and np.array_equal(ids, ido)
     return sc, ids
 
@@ -48,8 +53,9 @@ def test_dynamic_dense_vs_oracle(genome_case):
     nb[::4, 9] = c["nwin"] + 17          # past the genome end: kept, empty window
     nb[::5, 11] = c["nwin"] - 1          # the last reverse-complement window
     t = GenomeTable(c["g"], 150)
-    sc, ids = _both(t, c["g"], nb, c["q"], c["ql"], 1, 128, 160)
-    assert (ids == np.uint64(2 ** 64 - 1)).any()
+    _both(t, c["g"], nb, c["q"], c["ql"], 1, 128, 160)
+    sc, ids = _both(t, c["g"], nb, c["q"], c["ql"], 1, 160, 160)  # k = all: the empty windows are kept, score 0
+    assert (ids == np.uint64(2 ** 64 - 1)).any() and (sc[ids == np.uint64(2 ** 64 - 1)] == 0).all()
     _both(t, c["g"], nb, c["q"], c["ql"], 1, 5, 5)
     t.free()
 
@@ -63,7 +69,8 @@ def test_dynamic_sparse_vs_oracle(genome_case, stride):
     nb[::7, 0] = -1
     t = GenomeTable(c["g"], 150)
     _both(t, c["g"], nb, c["q"], c["ql"], stride, 5, 5)
-    _both(t, c["g"], nb, c["q"], c["ql"], stride, 64, 20)
+    _both(t, c["g"], nb, c["q"], c["ql"], stride, 32, 20)
+    _both(t, c["g"], nb, c["q"], c["ql"], stride, 64, 20)  # stride 2: 20 x 3 < 64 -> the reference's error
     t.free()
 
 

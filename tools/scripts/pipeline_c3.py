@@ -32,3 +32,4 @@ for rep in range(2):
         sys.exit(1)
     print(f"run {rep}: wall {time.time() - t0:.1f} s")
     print("\n".join(l for l in r.stdout.split("\n") if "time" in l.lower()), flush=True)
+    print("\n".join(l for l in r.stderr.split("\n") if l.startswith("[exec]")), flush=True)
