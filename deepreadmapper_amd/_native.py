@@ -35,7 +35,7 @@ EXPORTS = [
     "drm_multi_free", "drm_multi_get_index_info", "drm_multi_search_rerank", "drm_comm_unique_id", "drm_comm_init",
     "drm_comm_free", "drm_comm_gather_rows", "drm_refs_create_genome", "drm_refs_is_genome",
     "drm_extract_fasta_sequence", "drm_post_process_sw_dynamic", "drm_post_process_sw_dynamic_device",
-    "drm_multi_create_genome",
+    "drm_multi_create_genome", "drm_search_rerank_prepare",
 ]
 
 
@@ -140,6 +140,7 @@ def lib():
         "drm_refs_create_genome": (C.c_int, [vp, i64, i32, C.c_int, C.POINTER(vp)]),
         "drm_refs_is_genome": (C.c_int, [vp, C.POINTER(C.c_int)]),
         "drm_multi_create_genome": (C.c_int, [C.c_char_p, vp, C.c_int, vp, i64, i32, C.POINTER(vp)]),
+        "drm_search_rerank_prepare": (C.c_int, [vp, i64, i32, i32, i32, i32]),
         "drm_extract_fasta_sequence": (C.c_int, [C.c_char_p, vp, C.POINTER(i64)]),
         "drm_post_process_sw_dynamic": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
                                                   C.POINTER(i64)]),

@@ -81,8 +81,12 @@ struct DevMem {
 };
 
 // One device buffer set of the batch pipeline.
+struct Span {
+    void *p = nullptr;
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
 struct BatchSet {
-    std::unique_ptr<DevMem> x, q, ql, D, I, nd, nh, sc, id, st;
+    Span x, q, ql, D, I, nd, nh, sc, id, st; // slices of the cache's one device arena
     hipEvent_t in_done = nullptr, search_done = nullptr, comp_done = nullptr, out_done = nullptr;
     bool busy = false;
 };
@@ -98,6 +102,21 @@ struct ExecCache {
     BatchSet sets[kSets];
     int64_t B = 0, d = 0, kc = 0, kr = 0, q_stride = 0;
     bool rr = false;
+    std::unique_ptr<DevMem> arena;
+    // pinned host staging of the per-query ndis / nhops (a copy into pageable memory would block the
+    // host thread until the kernels before it finish, serialising the batch loop)
+    int32_t *h_stats = nullptr;
+    int64_t h_stats_n = 0;
+    void reserve_stats(int64_t n)
+    {
+        if (n <= h_stats_n)
+            return;
+        if (h_stats)
+            HC(hipHostFree(h_stats));
+        h_stats = nullptr;
+        HC(hipHostMalloc((void **)&h_stats, sizeof(int32_t) * 2 * (size_t)n, hipHostMallocDefault));
+        h_stats_n = n;
+    }
 
     void init(int dev)
     {
@@ -121,18 +140,24 @@ struct ExecCache {
         kr = std::max(kr, kr_);
         q_stride = std::max(q_stride, qs_);
         rr = rr || rr_;
+        // one allocation for all sets (each hipMalloc maps its pages up front; ten per set cost ms)
+        const size_t qsz = (size_t)std::max<int64_t>(q_stride, 1), ksz = (size_t)std::max<int64_t>(kr, 1);
+        const size_t sizes[10] = {sizeof(float) * (size_t)B * d, sizeof(float) * (size_t)B * kc,
+                                  sizeof(int64_t) * (size_t)B * kc, sizeof(int32_t) * (size_t)B,
+                                  sizeof(int32_t) * (size_t)B, rr ? (size_t)B * qsz : 0,
+                                  rr ? sizeof(int32_t) * (size_t)B : 0, rr ? sizeof(int32_t) * (size_t)B * ksz : 0,
+                                  rr ? sizeof(uint64_t) * (size_t)B * ksz : 0, rr ? sizeof(int32_t) * (size_t)B : 0};
+        size_t per_set = 0;
+        for (size_t z : sizes)
+            per_set += (z + 255) & ~(size_t)255;
+        arena.reset(); // release the old arena first (the sets are idle between calls)
+        arena.reset(new DevMem(per_set * kSets));
+        uint8_t *base = arena->as<uint8_t>();
         for (auto &s : sets) {
-            s.x.reset(new DevMem(sizeof(float) * (size_t)B * d));
-            s.D.reset(new DevMem(sizeof(float) * (size_t)B * kc));
-            s.I.reset(new DevMem(sizeof(int64_t) * (size_t)B * kc));
-            s.nd.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-            s.nh.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-            if (rr) {
-                s.q.reset(new DevMem((size_t)B * std::max<int64_t>(q_stride, 1)));
-                s.ql.reset(new DevMem(sizeof(int32_t) * (size_t)B));
-                s.sc.reset(new DevMem(sizeof(int32_t) * (size_t)B * std::max<int64_t>(kr, 1)));
-                s.id.reset(new DevMem(sizeof(uint64_t) * (size_t)B * std::max<int64_t>(kr, 1)));
-                s.st.reset(new DevMem(sizeof(int32_t) * (size_t)B));
+            Span *dst[10] = {&s.x, &s.D, &s.I, &s.nd, &s.nh, &s.q, &s.ql, &s.sc, &s.id, &s.st};
+            for (int i = 0; i < 10; ++i) {
+                dst[i]->p = sizes[i] ? base : nullptr;
+                base += (sizes[i] + 255) & ~(size_t)255;
             }
         }
     }
@@ -160,6 +185,8 @@ struct ExecCache {
         for (hipStream_t s : {s_in, s_search, s_sw, s_out})
             if (s)
                 (void)hipStreamDestroy(s);
+        if (h_stats)
+            (void)hipHostFree(h_stats);
     }
 };
 
@@ -248,9 +275,10 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
     const int64_t B = std::min<int64_t>(n, batch_size_for(n));
     const size_t kc = (size_t)k_clusters, kr = rr ? (size_t)k : 0;
     ExecCache &ex = exec_for(index, info.device);
-    std::vector<int32_t> nd_host((size_t)n), nh_host((size_t)n);
     try {
         ex.reserve(B, d, (int64_t)kc, (int64_t)kr, rr ? q_stride : 0, rr);
+        ex.reserve_stats(n);
+        int32_t *nd_host = ex.h_stats, *nh_host = ex.h_stats + n;
         if (verbose)
             std::fprintf(stderr, "[exec] %lld queries, batch %lld: setup %.2f ms\n", (long long)n, (long long)B, ms_since());
         HC(hipEventRecord(ex.e0, ex.s_search));
@@ -263,42 +291,48 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             const int64_t nb = std::min(B, n - lo);
             const size_t m = (size_t)nb;
             // host -> device (s_in)
-            HC(hipMemcpyAsync(s.x->p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_in));
+            HC(hipMemcpyAsync(s.x.p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_in));
             if (rr) {
-                HC(hipMemcpyAsync(s.q->p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice,
+                HC(hipMemcpyAsync(s.q.p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice,
                                   ex.s_in));
-                HC(hipMemcpyAsync(s.ql->p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_in));
+                HC(hipMemcpyAsync(s.ql.p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_in));
             }
             HC(hipEventRecord(s.in_done, ex.s_in));
+            if (verbose)
+                std::fprintf(stderr, "[exec]   b%lld copies in %.2f ms\n", (long long)b, ms_since());
             // search (s_search), then rerank (s_sw): the next batch's search may start while this batch's
             // rerank drains, filling the CUs its persistent grid leaves idle
             HC(hipStreamWaitEvent(ex.s_search, s.in_done, 0));
-            abi_check(drm_search_device_ex(index, s.x->as<float>(), nb, k_clusters, ef, s.D->as<float>(),
-                                           s.I->as<int64_t>(), s.nd->as<int32_t>(), s.nh->as<int32_t>(), nullptr,
+            abi_check(drm_search_device_ex(index, s.x.as<float>(), nb, k_clusters, ef, s.D.as<float>(),
+                                           s.I.as<int64_t>(), s.nd.as<int32_t>(), s.nh.as<int32_t>(), nullptr,
                                            ex.s_search));
             HC(hipEventRecord(s.search_done, ex.s_search));
+            if (verbose)
+                std::fprintf(stderr, "[exec]   b%lld search %.2f ms\n", (long long)b, ms_since());
             hipStream_t s_last = ex.s_search;
             if (rr) {
                 HC(hipStreamWaitEvent(ex.s_sw, s.search_done, 0));
                 auto *pp = genome_mode ? drm_post_process_sw_dynamic_device : drm_post_process_sw_static_device;
-                abi_check(pp(refs, s.I->as<int64_t>(), nb, k_clusters, s.q->as<uint8_t>(), s.ql->as<int32_t>(), q_stride,
-                             stride, k, k_clusters, s.sc->as<int32_t>(), s.id->as<uint64_t>(), s.st->as<int32_t>(),
+                abi_check(pp(refs, s.I.as<int64_t>(), nb, k_clusters, s.q.as<uint8_t>(), s.ql.as<int32_t>(), q_stride,
+                             stride, k, k_clusters, s.sc.as<int32_t>(), s.id.as<uint64_t>(), s.st.as<int32_t>(),
                              ex.s_sw));
                 s_last = ex.s_sw;
             }
             HC(hipEventRecord(s.comp_done, s_last));
+            if (verbose)
+                std::fprintf(stderr, "[exec]   b%lld rerank %.2f ms\n", (long long)b, ms_since());
             // device -> host (s_out)
             HC(hipStreamWaitEvent(ex.s_out, s.comp_done, 0));
-            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D->p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I->p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(nd_host.data() + lo, s.nd->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(nh_host.data() + lo, s.nh->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D.p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I.p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(nd_host + lo, s.nd.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipMemcpyAsync(nh_host + lo, s.nh.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
             if (rr) {
-                HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc->p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
+                HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc.p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
                                   ex.s_out));
-                HC(hipMemcpyAsync(sw_ids + (size_t)lo * kr, s.id->p, sizeof(uint64_t) * m * kr, hipMemcpyDeviceToHost,
+                HC(hipMemcpyAsync(sw_ids + (size_t)lo * kr, s.id.p, sizeof(uint64_t) * m * kr, hipMemcpyDeviceToHost,
                                   ex.s_out));
-                HC(hipMemcpyAsync(status + lo, s.st->p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
+                HC(hipMemcpyAsync(status + lo, s.st.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
             }
             HC(hipEventRecord(s.out_done, ex.s_out));
             if (verbose)
@@ -318,8 +352,8 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             stats->ndis = 0;
             stats->nhops = 0;
             for (int64_t i = 0; i < n; ++i) {
-                stats->ndis += nd_host[(size_t)i];
-                stats->nhops += nh_host[(size_t)i];
+                stats->ndis += nd_host[i];
+                stats->nhops += nh_host[i];
             }
             stats->kernel_ms = ms; // device span from the first search to the last rerank
         }
@@ -359,6 +393,25 @@ int drm_host_free(void *ptr)
     return guard([&] {
         if (ptr)
             HC(hipHostFree(ptr));
+    });
+}
+
+int drm_search_rerank_prepare(drm_index *index, int64_t n, int32_t d, int32_t k_clusters, int32_t k, int32_t q_stride)
+{
+    return guard([&] {
+        if (!index || n <= 0 || d <= 0 || k_clusters <= 0)
+            throw Error(DRM_ERR_ARG, "invalid prepare arguments");
+        drm_index_info info;
+        abi_check(drm_index_get_info(index, &info));
+        HC(hipSetDevice(info.device));
+        ExecCache &ex = exec_for(index, info.device);
+        const bool rr = q_stride > 0;
+        ex.reserve(std::min<int64_t>(n, batch_size_for(n)), d, k_clusters, rr ? k : 0, q_stride, rr);
+        ex.reserve_stats(n);
+        // first use of the copy queues and the arena: a small round trip on both copy streams
+        HC(hipMemcpyAsync(ex.sets[0].nd.p, ex.h_stats, sizeof(int32_t), hipMemcpyHostToDevice, ex.s_in));
+        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].nd.p, sizeof(int32_t), hipMemcpyDeviceToHost, ex.s_out));
+        ex.drain();
     });
 }
 

@@ -218,6 +218,10 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
                       int32_t k, float *D, int64_t *I, int32_t *sw_scores, uint64_t *sw_ids, int32_t *status,
                       drm_search_stats *stats);
 
+/* Optional: set up drm_search_rerank's streams and device buffers for a batch of n queries ahead of the
+ * call (q_stride = 0: search only), so the call itself only streams data and runs kernels. */
+int drm_search_rerank_prepare(drm_index *index, int64_t n, int32_t d, int32_t k_clusters, int32_t k, int32_t q_stride);
+
 /* ---------------------------------------------------------------- multi-GPU fan-out
  * One index replica (and window table, when windows != NULL) per entry of devices[ndev] -- the same
  * device may appear more than once. drm_multi_search_rerank splits the n queries into contiguous
