@@ -235,6 +235,35 @@ def prepare_c5(args, D, dev):
                     f"GPU-built), replicated per GPU, {Q} reads per GPU, search + SW rerank, EF=128 K=128"}
 
 
+def host_path(ix, table, q_emb, queries, K, EF, flat):
+    """The drop-in boundary's own rate (not `value`): drm_search_rerank from pinned host buffers to pinned
+    host outputs -- PCIe transfers in, kernels, PCIe transfers out, batches overlapped (exec.cpp) --
+    timed once after one warm call, on this rank's reads."""
+    if flat:
+        return None
+    from deepreadmapper_amd.executor import pinned_empty, prepare, search_rerank
+    n = len(q_emb)
+    x = pinned_empty(q_emb.shape, np.float32)
+    x[...] = q_emb
+    qb = pinned_empty(queries.shape, np.uint8)
+    qb[...] = queries
+    ql = pinned_empty((n,), np.int32)
+    ql[...] = queries.shape[1]
+    out = {"D": pinned_empty((n, K), np.float32), "I": pinned_empty((n, K), np.int64),
+           "sw_scores": pinned_empty((n, K), np.int32), "sw_ids": pinned_empty((n, K), np.uint64),
+           "status": pinned_empty((n,), np.int32)}
+    bytes_io = x.nbytes + qb.nbytes + ql.nbytes + sum(v.nbytes for v in out.values())
+    prepare(ix, n, q_emb.shape[1], K, K, queries.shape[1])
+    search_rerank(ix, table, x, (qb, ql), k=K, ef=EF, out=out)
+    t0 = time.perf_counter()
+    o = search_rerank(ix, table, x, (qb, ql), k=K, ef=EF, out=out)
+    ms = (time.perf_counter() - t0) * 1e3
+    return {"value": round(n / (ms * 1e-3), 1), "unit": "reads/s", "ms": round(ms, 2),
+            "device_span_ms": round(o["stats"].kernel_ms, 2), "pcie_bytes": int(bytes_io),
+            "status_ok": bool((o["status"] == K).all()),
+            "note": "drm_search_rerank, pinned host in/out, one rank, PCIe-inclusive (not the metric)"}
+
+
 def gather_results(D, dev, n_total, bufs, local_host):
     """End-of-run exchange: every rank's device-resident result rows are gathered to
     rank 0 over RCCL by the library's own C++ path (drm_comm_gather_rows: grouped ncclSend/ncclRecv over
@@ -376,6 +405,7 @@ def main():
     ap.add_argument("--cache", default=os.environ.get("DRM_BENCH_CACHE", "/tmp/drm_bench_cache"))
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the pinned-host drm_search_rerank timing")
     ap.add_argument("--build-threads", type=int, default=0)
     ap.add_argument("--index", choices=["pq", "flat"], default="pq",
                     help="pq (default): faiss IndexHNSWPQ, the live pipeline's index (src/main.cpp:236-237); flat: "
@@ -511,6 +541,8 @@ def main():
     # VALU issue ceiling of the SW DP: 4 SIMD x 16 lanes per CU, 2 cells per packed lane-op
     sw_peak_gcups = ncu * 64 * CLOCK_HZ / SW_VALU_PER_CELL / 1e9
 
+    host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
+
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
     gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_L if flat else d_I),
@@ -553,6 +585,7 @@ def main():
                             if sw_pmc and "valu_issue_frac" in sw_pmc else None},
             "cpu_baseline": cpu,
             "gather": gather,
+            "host_path": host,
             "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),

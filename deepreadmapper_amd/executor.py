@@ -34,13 +34,46 @@ def _query_args(x, queries):
     return x, qbuf, ql, qbuf.shape[1]
 
 
-def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None, stride=1):
+class _Pinned:
+    def __init__(self, nbytes):
+        p = C.c_void_p()
+        check(lib().drm_host_alloc(C.byref(p), max(int(nbytes), 1)))
+        self.ptr = p.value
+
+    def __del__(self):
+        try:
+            lib().drm_host_free(self.ptr)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def pinned_empty(shape, dtype):
+    """A numpy array in pinned host memory (drm_host_alloc): the executor's copies to and from it are
+    DMA transfers that overlap the kernels. The array keeps its allocation alive."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64))
+    buf = _Pinned(n * dtype.itemsize)
+    raw = (C.c_uint8 * max(n * dtype.itemsize, 1)).from_address(buf.ptr)
+    a = np.frombuffer(raw, dtype=np.uint8, count=n * dtype.itemsize).view(dtype).reshape(shape)
+    _KEEP.append(buf)  # pinned buffers live as long as the process (the bench's few large arrays)
+    return a
+
+
+_KEEP = []
+
+
+def prepare(index, n, d, k_clusters, k=0, q_stride=0):
+    """drm_search_rerank_prepare: streams and device buffers for a batch of n queries, ahead of the call."""
+    check(lib().drm_search_rerank_prepare(index.handle, int(n), int(d), int(k_clusters), int(k), int(q_stride)))
+
+
+def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None, stride=1, out=None):
     """drm_search_rerank: search (k_clusters results) then, when `table` (WindowTable) and `queries`
     are given, the SW rerank to k. Returns a dict of D, I (+ sw_scores, sw_ids, status) and stats."""
     kc = k if k_clusters is None else k_clusters
     x, qbuf, ql, qs = _query_args(x, queries)
     rr = table is not None and qbuf is not None
-    o = _outputs(len(x), kc, k, rr)
+    o = out if out is not None else _outputs(len(x), kc, k, rr)
     st = SearchStats()
     check(lib().drm_search_rerank(index.handle, table.handle if rr else None, ptr(x), len(x), x.shape[1], int(kc),
                                   int(ef), ptr(qbuf) if rr else None, ptr(ql) if rr else None, qs, int(stride),

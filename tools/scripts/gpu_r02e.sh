@@ -1,0 +1,10 @@
+#!/bin/bash
+# full validation: GPU test suite, smoke(), default bench (C5, CPU baseline, host path)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_r02e.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests_r02e.log; exit 1; }
+tail -3 gpurun_out/gpu_tests_r02e.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_r02e.log 2>&1 || { echo SMOKE_FAILED; tail -20 gpurun_out/smoke_r02e.log; exit 1; }
+tail -2 gpurun_out/smoke_r02e.log
+timeout -k 10 900 python -u bench.py > gpurun_out/bench_r02e_c5.json 2> gpurun_out/bench_r02e_c5.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench_r02e_c5.err; exit 1; }
+cat gpurun_out/bench_r02e_c5.json
