@@ -16,9 +16,9 @@ HOSTFLAGS := $(COMMON) -fopenmp -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I$(ROC
 
 LIB := $(PKG)/libdrm_hip.so
 HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/hnsw_pq_fast.o $(BUILD)/builder_gpu.o $(BUILD)/embed_gpu.o $(BUILD)/hnsw_search_lds.o $(BUILD)/hnsw_flat_search.o $(BUILD)/sw_rerank.o \
-            $(BUILD)/capi.o $(BUILD)/exec.o
+            $(BUILD)/encoder_gru.o $(BUILD)/capi.o $(BUILD)/exec.o
 HOST_OBJS := $(BUILD)/faiss_io.o $(BUILD)/formats.o $(BUILD)/builder.o $(BUILD)/embed.o $(BUILD)/hnswlib_io.o \
-             $(BUILD)/builder_flat.o
+             $(BUILD)/builder_flat.o $(BUILD)/encoder.o
 HDRS := include/drm_hip.h $(SRC)/drm_internal.h $(SRC)/drm_device.h $(SRC)/pq_common.h
 
 all: $(LIB) bin/pipeline bin/hnswpq_index oracle

@@ -11,3 +11,4 @@ from .rerank import (WindowTable, calc_sw_score, calc_sw_scores, post_process_sw
 
 __version__ = "0.1.0"
 from .executor import Comm, MultiIndex, search_rerank  # noqa: F401  (batch executor, multi-GPU, RCCL gather)
+from .encoder import Encoder, Preprocessor, Vectorizer, export_encoder  # noqa: F401  (GRU read encoder)

@@ -36,6 +36,8 @@ EXPORTS = [
     "drm_comm_free", "drm_comm_gather_rows", "drm_refs_create_genome", "drm_refs_is_genome",
     "drm_extract_fasta_sequence", "drm_post_process_sw_dynamic", "drm_post_process_sw_dynamic_device",
     "drm_multi_create_genome", "drm_search_rerank_prepare",
+    "drm_encoder_load", "drm_encoder_export", "drm_encoder_free", "drm_encoder_get_info", "drm_tokenize",
+    "drm_vectorize", "drm_vectorize_device", "drm_encoder_flags",
 ]
 
 
@@ -58,6 +60,11 @@ class FlatIndexInfo(C.Structure):
     _fields_ = [("d", C.c_int32), ("ntotal", C.c_int64), ("M", C.c_int32), ("maxM0", C.c_int32),
                 ("maxM", C.c_int32), ("max_level", C.c_int32), ("entry_point", C.c_uint32),
                 ("efConstruction", C.c_int32), ("device_bytes", C.c_int64)]
+
+
+class EncoderInfo(C.Structure):
+    _fields_ = [("hidden", C.c_int32), ("emb_dim", C.c_int32), ("max_len", C.c_int32), ("out_dim", C.c_int32),
+                ("n_token_rows", C.c_int32), ("device", C.c_int32), ("h0", C.c_float), ("device_bytes", C.c_int64)]
 
 
 class SearchStats(C.Structure):
@@ -146,6 +153,14 @@ def lib():
                                                   C.POINTER(i64)]),
         "drm_post_process_sw_dynamic_device": (C.c_int, [vp, vp, i64, i32, vp, vp, i32, i64, i32, i32, vp, vp, vp,
                                                          vp]),
+        "drm_encoder_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
+        "drm_encoder_export": (C.c_int, [C.c_char_p, C.c_char_p]),
+        "drm_encoder_free": (C.c_int, [vp]),
+        "drm_encoder_get_info": (C.c_int, [vp, C.POINTER(EncoderInfo)]),
+        "drm_tokenize": (C.c_int, [vp, vp, vp, i64, i64, vp]),
+        "drm_vectorize": (C.c_int, [vp, vp, vp, i64, i64, vp, C.POINTER(i64)]),
+        "drm_vectorize_device": (C.c_int, [vp, vp, vp, i64, i64, vp, vp]),
+        "drm_encoder_flags": (C.c_int, [vp, C.POINTER(i64), C.POINTER(i64)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -26,6 +26,9 @@ struct drm_refs {
 struct drm_flat_index {
     drm::DeviceFlatIndex dev;
 };
+struct drm_encoder {
+    drm::DeviceEncoder dev;
+};
 
 using drm::Error;
 
@@ -940,3 +943,124 @@ int drm_post_process_sw_dynamic(drm_refs *refs, const int64_t *neighbors, int64_
 }
 
 } // extern "C"
+
+// ------------------------------------------------------------------------------- read encoder
+static void check_seqs(const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride)
+{
+    if (n < 0 || (n > 0 && (!seqs || !lens)) || stride <= 0) throw Error(DRM_ERR_ARG, "invalid sequence batch");
+    for (int64_t i = 0; i < n; ++i)
+        if (lens[i] < 2 || lens[i] > stride)
+            throw Error(DRM_ERR_ARG, "sequence " + std::to_string(i) + " has length " + std::to_string(lens[i]) +
+                                         " (need 2 <= len <= stride)");
+}
+
+extern "C" int drm_encoder_load(const char *model_path, int device, drm_encoder **out)
+{
+    return guarded([&] {
+        if (!model_path || !out) throw Error(DRM_ERR_ARG, "null argument");
+        drm::EncoderHost h = drm::read_encoder(model_path);
+        auto e = std::make_unique<drm_encoder>();
+        try {
+            drm::encoder_upload(e->dev, h, device);
+        } catch (...) {
+            drm::encoder_release(e->dev);
+            throw;
+        }
+        if (const char *v = getenv("DRM_ENC_TILES")) e->dev.max_tiles_per_launch = std::max(1, atoi(v));
+        *out = e.release();
+    });
+}
+
+extern "C" int drm_encoder_export(const char *model_path, const char *out_path)
+{
+    return guarded([&] {
+        if (!model_path || !out_path) throw Error(DRM_ERR_ARG, "null argument");
+        drm::write_encoder(drm::read_encoder(model_path), out_path);
+    });
+}
+
+extern "C" int drm_encoder_free(drm_encoder *enc)
+{
+    return guarded([&] {
+        if (!enc) return;
+        drm::encoder_release(enc->dev);
+        delete enc;
+    });
+}
+
+extern "C" int drm_encoder_get_info(const drm_encoder *enc, drm_encoder_info *info)
+{
+    return guarded([&] {
+        if (!enc || !info) throw Error(DRM_ERR_ARG, "null argument");
+        *info = drm_encoder_info{64, 64, 123, 128, 1 + drm::kTokenHashes, enc->dev.device, enc->dev.h0,
+                                 enc->dev.device_bytes + enc->dev.y1_tiles * drm::encoder_tile_bytes()};
+    });
+}
+
+extern "C" int drm_tokenize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride,
+                            int32_t *tokens)
+{
+    return guarded([&] {
+        if (!enc || (n > 0 && !tokens)) throw Error(DRM_ERR_ARG, "null argument");
+        check_seqs(seqs, lens, n, stride);
+        if (n == 0) return;
+        DRM_HIP_CHECK(hipSetDevice(enc->dev.device));
+        DevBuf<uint8_t> d_s(n * stride);
+        DevBuf<int32_t> d_l(n), d_t(n * 123);
+        DRM_HIP_CHECK(hipMemcpy(d_s.p, seqs, n * stride, hipMemcpyHostToDevice));
+        DRM_HIP_CHECK(hipMemcpy(d_l.p, lens, n * 4, hipMemcpyHostToDevice));
+        drm::launch_tokenize(enc->dev, d_s.p, d_l.p, n, stride, d_t.p, nullptr);
+        DRM_HIP_CHECK(hipMemcpy(tokens, d_t.p, n * 123 * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+static void read_flags(drm_encoder *enc, int64_t *undef, int64_t *shorts)
+{
+    uint32_t f[2];
+    DRM_HIP_CHECK(hipMemcpy(f, enc->dev.flags, 8, hipMemcpyDeviceToHost));
+    DRM_HIP_CHECK(hipMemset(enc->dev.flags, 0, 8));
+    if (undef) *undef = f[0];
+    if (shorts) *shorts = f[1];
+}
+
+extern "C" int drm_vectorize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride,
+                             float *out, int64_t *n_undefined)
+{
+    return guarded([&] {
+        if (!enc || (n > 0 && !out)) throw Error(DRM_ERR_ARG, "null argument");
+        check_seqs(seqs, lens, n, stride);
+        if (n_undefined) *n_undefined = 0;
+        if (n == 0) return;
+        DRM_HIP_CHECK(hipSetDevice(enc->dev.device));
+        DevBuf<uint8_t> d_s(n * stride);
+        DevBuf<int32_t> d_l(n);
+        DevBuf<float> d_o(n * 128);
+        DRM_HIP_CHECK(hipMemcpy(d_s.p, seqs, n * stride, hipMemcpyHostToDevice));
+        DRM_HIP_CHECK(hipMemcpy(d_l.p, lens, n * 4, hipMemcpyHostToDevice));
+        read_flags(enc, nullptr, nullptr);
+        drm::launch_encode(enc->dev, d_s.p, d_l.p, n, stride, d_o.p, nullptr);
+        DRM_HIP_CHECK(hipMemcpy(out, d_o.p, n * 128 * 4, hipMemcpyDeviceToHost));
+        read_flags(enc, n_undefined, nullptr);
+    });
+}
+
+extern "C" int drm_vectorize_device(drm_encoder *enc, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n,
+                                    int64_t stride, float *d_out, void *stream)
+{
+    return guarded([&] {
+        if (!enc || n < 0 || stride <= 0 || (n > 0 && (!d_seqs || !d_lens || !d_out)))
+            throw Error(DRM_ERR_ARG, "invalid argument");
+        DRM_HIP_CHECK(hipSetDevice(enc->dev.device));
+        drm::launch_encode(enc->dev, d_seqs, d_lens, n, stride, d_out, (hipStream_t)stream);
+    });
+}
+
+extern "C" int drm_encoder_flags(drm_encoder *enc, int64_t *n_undefined, int64_t *n_short)
+{
+    return guarded([&] {
+        if (!enc) throw Error(DRM_ERR_ARG, "null argument");
+        DRM_HIP_CHECK(hipSetDevice(enc->dev.device));
+        DRM_HIP_CHECK(hipDeviceSynchronize());
+        read_flags(enc, n_undefined, n_short);
+    });
+}

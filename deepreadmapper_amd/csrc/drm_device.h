@@ -236,4 +236,27 @@ void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *
                      const int64_t *d_off2, const int32_t *d_len2, int64_t npairs, int32_t *d_scores, int max_len2,
                      hipStream_t stream);
 
+// ---------------------------------------------------------------------------------- read encoder
+// HBM image of the GRU read encoder (encoder_gru.hip)
+struct DeviceEncoder {
+    int device = 0;
+    float h0 = 0.f;
+    uint16_t *emb = nullptr;   // [97][64] f16: row 0 = padding id 0, row 1 + h = _Tok2Index[h]
+    uint16_t *vocab = nullptr; // [97] vocabulary id per row (drm_tokenize output)
+    uint16_t *W[2] = {}, *R[2] = {}; // f16 [2 dirs][192][in], [2][192][64] (gate order z, r, n)
+    float *B[2] = {};          // [2][256] f32: b_z, b_r, Wb_n, Rb_n
+    uint16_t *y1 = nullptr;    // layer-1 outputs of the tiles in flight (hi/lo f16), grown on demand
+    int64_t y1_tiles = 0;
+    int64_t max_tiles_per_launch = 2048; // 32 reads each; 2 MB of layer-1 output per tile (DRM_ENC_TILES)
+    uint32_t *flags = nullptr; // [0] tokens past _Tok2Index, [1] sequences shorter than 2 bytes
+    int64_t device_bytes = 0;
+};
+int64_t encoder_tile_bytes();
+void encoder_upload(DeviceEncoder &d, const EncoderHost &h, int device);
+void encoder_release(DeviceEncoder &d);
+void launch_encode(DeviceEncoder &d, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
+                   float *d_out, hipStream_t stream);
+void launch_tokenize(const DeviceEncoder &d, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
+                     int32_t *d_tokens, hipStream_t stream);
+
 } // namespace drm

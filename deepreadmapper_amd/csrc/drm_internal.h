@@ -149,4 +149,22 @@ void embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len, in
 std::vector<double> kmer3_matrix(int dim, uint64_t seed);
 constexpr uint64_t kEmbedSeed = 42; // seed of the stand-in embedder used by the CLIs
 
+// ---------------------------------------------------------------------------------------------
+// Read encoder (encoder.cpp): the reference's OpenVINO GRU model (models/finetuned_sgn33-new-a-Apr6.xml,
+// src/inference/fast_model.cpp), f16 tensors as the IR stores them.
+// ---------------------------------------------------------------------------------------------
+constexpr int kTokenHashes = 96; // hashToken range backed by _Tok2Index (includes/inference/preprocess.hpp:32-49)
+
+struct EncoderHost {
+    int32_t hidden = 64, emb_dim = 64, max_len = 123; // config.hpp:21 (MAX_LEN), the IR's GRU/embedding sizes
+    float h0 = 0.f;
+    std::vector<uint16_t> vocab_rows; // [1 + 96] vocabulary id of each embedding row (token_vocab_rows)
+    std::vector<uint16_t> emb_rows;   // [rows][emb_dim] f16 bits
+    std::vector<uint16_t> W[2], R[2], B[2]; // f16 bits: W [2][3H][in], R [2][3H][H], B [2][4H] (zrh)
+    int in_dim(int layer) const { return layer == 0 ? emb_dim : 2 * hidden; }
+};
+std::vector<uint16_t> token_vocab_rows();
+EncoderHost read_encoder(const std::string &path); // .xml (IR + sibling .bin) or .drmenc; throws Error
+void write_encoder(const EncoderHost &e, const std::string &path);
+
 } // namespace drm

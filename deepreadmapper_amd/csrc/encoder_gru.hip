@@ -1,0 +1,416 @@
+// deepreadmapper_amd/csrc/encoder_gru.hip -- the read encoder on gfx950:
+// Vectorizer::vectorize (src/inference/vectorize.cpp:34-141) = Preprocessor tokens
+// (src/inference/preprocess.cpp:20-42) -> embedding -> 2 x bidirectional GRU (hidden 64,
+// linear_before_reset) -> concat(final fwd h, final bwd h) of layer 2, as the IR
+// models/finetuned_sgn33-new-a-Apr6.xml runs it under OpenVINO (src/inference/fast_model.cpp).
+//
+// One workgroup = one tile of 32 reads, 8 waves: waves 0-3 run the forward direction, 4-7 the
+// backward one, wave w owning hidden units [16(w&3), +16). Each recurrence step is a [32 x K] x [K x 16]
+// product per gate on the 16x16x32 f16 MFMA: the weights are f16 in the IR (exact B operands, held in
+// VGPRs for the whole layer); the f32 state h enters as two f16 terms hi = f16(h), lo = f16(h - hi)
+// (~22 significant bits, f32 accumulation), so the recurrence stays f32-grade at the f16 matrix rate.
+// Layer 1's input x_t is the token's embedding row (f16-exact, K = 64, fused into the same chains);
+// layer 2's input is layer 1's output [fwd | bwd] at t, written to HBM as hi/lo f16 by layer 1 and
+// staged back through LDS one step ahead. Gate math per (read, unit):
+//   z = s(x Wz' + h Rz' + bz), r = s(x Wr' + h Rr' + br), n = tanh(x Wn' + Wbn + r (h Rn' + Rbn)),
+//   h' = n + z (h - n)                                       (OpenVINO GRUCell, linear_before_reset)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "drm_device.h"
+
+namespace drm {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kT = 32;   // reads per tile: two 16-row MFMA blocks
+constexpr int kL = 123;  // recurrence steps = Config::Inference::MAX_LEN (config.hpp:21)
+constexpr int kH = 64;   // hidden units
+constexpr int kHS = 72;  // LDS row stride (halfs) of h images: 144-B rows, conflict-free ds_read_b128
+constexpr int kES = 72;  // LDS row stride (halfs) of embedding rows
+constexpr int kXS = 264; // LDS row stride (halfs) of staged layer-1 outputs: 528-B rows
+constexpr int kYR = 256; // layer-1 output row in HBM: hi[fwd 64 | bwd 64] | lo[fwd 64 | bwd 64]
+constexpr int kRows = 1 + kTokenHashes;
+constexpr int kTokStride = 128;
+constexpr size_t kHbBytes = size_t(2) * 2 * 2 * kT * kHS * 2;  // [dir][buf][hi/lo] images
+constexpr size_t kXbBytes = size_t(2) * 2 * kT * kXS * 2;      // [dir][buf] staged inputs (layer 2)
+static_assert(kRows * kES * 2 <= 16384 && 16384 + kT * kTokStride <= kXbBytes, "layer-1 LDS carve");
+
+__device__ __forceinline__ int lower(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+
+__device__ __forceinline__ int cval(int c) // char2Val (preprocess.hpp:10-25), c lower-cased
+{
+    return c == 'a' ? 0 : c == 'c' ? 1 : c == 'g' ? 2 : c == 't' ? 3 : 7;
+}
+
+// hashToken (preprocess.hpp:32-49) of token t of a sequence of len >= 2 bytes, as
+// Preprocessor::preprocess places it (preprocess.cpp:25-40); -1 past the sequence's tokens
+__device__ __forceinline__ int token_hash(const uint8_t *s, int len, int t)
+{
+    const int n = min(kL, len);
+    if (t >= n) return -1;
+    int c0, c1, c2;
+    if (t == n - 1) { // result[len - 1]: seq[len-2], seq[len-1], then seq[len] or '>'
+        c0 = s[n - 2];
+        c1 = s[n - 1];
+        c2 = n < len ? s[n] : '>';
+    } else if (t == 0) { // result[0]: '<', seq[0], seq[1] (seq[0] is the tag itself in tagged reads)
+        c0 = '<';
+        c1 = s[0];
+        c2 = s[1];
+    } else {
+        c0 = s[t - 1];
+        c1 = s[t];
+        c2 = s[t + 1];
+    }
+    c0 = lower(c0);
+    c1 = lower(c1);
+    c2 = lower(c2);
+    if (c0 == '<') return (cval(c1) << 2) + cval(c2);
+    if (c2 == '>') return 16 + (cval(c0) << 2) + cval(c1);
+    return 32 + (cval(c0) << 4) + (cval(c1) << 2) + cval(c2);
+}
+
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_(float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; }
+
+__device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+
+struct EncArgs {
+    const uint8_t *seqs;
+    const int32_t *lens;
+    int64_t stride, n, first_tile;
+    const _Float16 *emb; // [kRows][64] (row 0 = padding id 0, row 1 + h = _Tok2Index[h])
+    const _Float16 *W1, *R1, *W2, *R2;
+    const float *B1, *B2; // [2][256] zrh: b_z, b_r, Wb_n, Rb_n
+    _Float16 *y1;         // [tiles of this launch][kL][kT][kYR]
+    float *out;           // [n][128]
+    float h0;
+    uint32_t *flags;      // [0] tokens past _Tok2Index (reference UB), [1] sequences shorter than 2
+};
+
+// Gate epilogue for one 16-row block: C layout col = lane & 15 (unit j), row = 4 (lane >> 4) + q.
+__device__ __forceinline__ void gates(const f4 &z, const f4 &r, const f4 &gx, const f4 &gh, float *hp, int row0, int j,
+                                      _Float16 *nh, _Float16 *nl)
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float zz = sigm(z[q]), rr = sigm(r[q]);
+        const float nn = tanh_(gx[q] + rr * gh[q]);
+        const float h = nn + zz * (hp[q] - nn);
+        hp[q] = h;
+        const _Float16 hi = (_Float16)h;
+        const _Float16 lo = (_Float16)(h - (float)hi);
+        nh[(row0 + q) * kHS + j] = hi;
+        nl[(row0 + q) * kHS + j] = lo;
+    }
+}
+
+__global__ __launch_bounds__(512) void gru_encode_kernel(EncArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kHbBytes + kXbBytes];
+    _Float16 *hb = (_Float16 *)smem;
+    uint8_t *xreg = smem + kHbBytes;
+    _Float16 *embs = (_Float16 *)xreg;
+    uint8_t *toks = xreg + 16384;
+    _Float16 *xb = (_Float16 *)xreg;
+
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int dir = wave >> 2, j = ((wave & 3) << 4) + (lane & 15), kq = lane >> 4, c16 = lane & 15;
+    const int dt = tid & 255; // thread index within the direction
+    const int64_t r0 = (a.first_tile + blockIdx.x) * kT;
+    _Float16 *y1 = a.y1 + (int64_t)blockIdx.x * kL * kT * kYR;
+    auto himg = [&](int d, int buf, int hl) { return hb + ((d * 2 + buf) * 2 + hl) * kT * kHS; };
+
+    // ---- tokens of the tile (row ids into the embedding rows) + embedding rows + h0 images
+    for (int i = tid; i < kT * kTokStride; i += 512) {
+        const int row = i / kTokStride, t = i % kTokStride;
+        const int64_t r = r0 + row;
+        int v = 0;
+        if (r < a.n && t < kL) {
+            const int len = a.lens[r];
+            if (len >= 2) {
+                const int h = token_hash(a.seqs + r * a.stride, len, t);
+                if (h >= kTokenHashes) atomicAdd(&a.flags[0], 1u);
+                v = (h >= 0 && h < kTokenHashes) ? h + 1 : 0;
+            } else if (t == 0) {
+                atomicAdd(&a.flags[1], 1u);
+            }
+        }
+        toks[i] = (uint8_t)v;
+    }
+    for (int i = tid; i < kRows * 8; i += 512)
+        *(h8 *)(embs + (i >> 3) * kES + (i & 7) * 8) = *(const h8 *)(a.emb + i * 8);
+    const _Float16 h0hi = (_Float16)a.h0, h0lo = (_Float16)(a.h0 - (float)h0hi);
+    auto init_h = [&]() {
+        for (int i = tid; i < 2 * kT * kH; i += 512) {
+            const int d = i / (kT * kH), row = (i / kH) % kT, c = i % kH;
+            himg(d, 0, 0)[row * kHS + c] = h0hi;
+            himg(d, 0, 1)[row * kHS + c] = h0lo;
+        }
+    };
+    init_h();
+
+    float hp[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hp[rb][q] = a.h0;
+
+    // ---------------------------------------------------------------- layer 1 (input = embedding)
+    {
+        const _Float16 *R = a.R1 + dir * 3 * kH * kH, *W = a.W1 + dir * 3 * kH * 64;
+        h8 rf[3][2], wf[3][2];
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
+                wf[g][c] = *(const h8 *)(W + (g * kH + j) * 64 + c * 32 + kq * 8);
+            }
+        const float *B = a.B1 + dir * 4 * kH;
+        const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
+        __syncthreads();
+        for (int s = 0; s < kL; ++s) {
+            const int t = dir ? kL - 1 - s : s, cur = s & 1;
+            const _Float16 *hh = himg(dir, cur, 0), *hl = himg(dir, cur, 1);
+            _Float16 *nh = himg(dir, cur ^ 1, 0), *nl = himg(dir, cur ^ 1, 1);
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const int ar = rb * 16 + c16;
+                const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
+                const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
+                const int tr = toks[ar * kTokStride + t];
+                const h8 ax0 = *(const h8 *)(embs + tr * kES + kq * 8), ax1 = *(const h8 *)(embs + tr * kES + 32 + kq * 8);
+                f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
+                z = mfma(ax0, wf[0][0], z);
+                r = mfma(ax0, wf[1][0], r);
+                gx = mfma(ax0, wf[2][0], gx);
+                gh = mfma(ah0, rf[2][0], gh);
+                z = mfma(ax1, wf[0][1], z);
+                r = mfma(ax1, wf[1][1], r);
+                gx = mfma(ax1, wf[2][1], gx);
+                gh = mfma(ah1, rf[2][1], gh);
+                z = mfma(ah0, rf[0][0], z);
+                r = mfma(ah0, rf[1][0], r);
+                gh = mfma(al0, rf[2][0], gh);
+                z = mfma(ah1, rf[0][1], z);
+                r = mfma(ah1, rf[1][1], r);
+                gh = mfma(al1, rf[2][1], gh);
+                z = mfma(al0, rf[0][0], z);
+                r = mfma(al0, rf[1][0], r);
+                z = mfma(al1, rf[0][1], z);
+                r = mfma(al1, rf[1][1], r);
+                gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
+            }
+            __syncthreads();
+            // this direction's h_t (hi, lo) -> HBM row t of layer 1's output
+            for (int c = dt; c < kT * 16; c += 256) {
+                const int row = c >> 4, hlsel = (c >> 3) & 1, seg = c & 7;
+                *(h8 *)(y1 + ((int64_t)t * kT + row) * kYR + hlsel * 128 + dir * kH + seg * 8) =
+                    *(const h8 *)((hlsel ? nl : nh) + row * kHS + seg * 8);
+            }
+        }
+    }
+    __syncthreads(); // layer-1 outputs of both directions written (workgroup-scope fence + barrier)
+
+    // ---------------------------------------------------------------- layer 2 (input = [fwd1 | bwd1])
+    {
+        const _Float16 *R = a.R2 + dir * 3 * kH * kH, *W = a.W2 + dir * 3 * kH * 2 * kH;
+        h8 rf[3][2], wf[3][4];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wf[g][c] = *(const h8 *)(W + (g * kH + j) * 2 * kH + c * 32 + kq * 8);
+        }
+        const float *B = a.B2 + dir * 4 * kH;
+        const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hp[rb][q] = a.h0;
+        // 32 rows x 512 B of layer-1 output per step and direction: 4 x 16 B per thread
+        h8 xr[4];
+        auto load_x = [&](int t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = dt + 256 * i, row = c >> 5, seg = c & 31;
+                xr[i] = *(const h8 *)(y1 + ((int64_t)t * kT + row) * kYR + seg * 8);
+            }
+        };
+        auto store_x = [&](int buf) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = dt + 256 * i, row = c >> 5, seg = c & 31;
+                *(h8 *)(xb + (dir * 2 + buf) * kT * kXS + row * kXS + seg * 8) = xr[i];
+            }
+        };
+        init_h();
+        load_x(dir ? kL - 1 : 0);
+        store_x(0);
+        __syncthreads();
+        for (int s = 0; s < kL; ++s) {
+            const int cur = s & 1;
+            if (s + 1 < kL) load_x(dir ? kL - 2 - s : s + 1);
+            const _Float16 *hh = himg(dir, cur, 0), *hl = himg(dir, cur, 1);
+            _Float16 *nh = himg(dir, cur ^ 1, 0), *nl = himg(dir, cur ^ 1, 1);
+            const _Float16 *xs = xb + (dir * 2 + cur) * kT * kXS;
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const int ar = rb * 16 + c16;
+                const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
+                const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
+                f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const h8 xh = *(const h8 *)(xs + ar * kXS + c * 32 + kq * 8);
+                    const h8 xl = *(const h8 *)(xs + ar * kXS + 128 + c * 32 + kq * 8);
+                    z = mfma(xh, wf[0][c], z);
+                    r = mfma(xh, wf[1][c], r);
+                    gx = mfma(xh, wf[2][c], gx);
+                    z = mfma(xl, wf[0][c], z);
+                    r = mfma(xl, wf[1][c], r);
+                    gx = mfma(xl, wf[2][c], gx);
+                }
+                gh = mfma(ah0, rf[2][0], gh);
+                z = mfma(ah0, rf[0][0], z);
+                r = mfma(ah0, rf[1][0], r);
+                gh = mfma(ah1, rf[2][1], gh);
+                z = mfma(ah1, rf[0][1], z);
+                r = mfma(ah1, rf[1][1], r);
+                gh = mfma(al0, rf[2][0], gh);
+                z = mfma(al0, rf[0][0], z);
+                r = mfma(al0, rf[1][0], r);
+                gh = mfma(al1, rf[2][1], gh);
+                z = mfma(al1, rf[0][1], z);
+                r = mfma(al1, rf[1][1], r);
+                gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
+            }
+            if (s + 1 < kL) store_x(cur ^ 1);
+            __syncthreads();
+        }
+    }
+    // final states of layer 2: [fwd | bwd] (the IR's Gather_6/7/8 + Concat)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t r = r0 + rb * 16 + kq * 4 + q;
+            if (r < a.n) a.out[r * 128 + dir * kH + j] = hp[rb][q];
+        }
+}
+
+// Preprocessor::preprocess + Vectorizer::prepareBatch's zero padding as model-input ids: one thread
+// per (sequence, position); -1 where the reference indexes past _Tok2Index.
+__global__ void tokenize_kernel(const uint8_t *seqs, const int32_t *lens, int64_t stride, int64_t n,
+                                const uint16_t *vocab, int32_t *tokens)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * kL) return;
+    const int64_t r = i / kL;
+    const int t = int(i % kL);
+    const int len = lens[r];
+    int v = 0;
+    if (len >= 2) {
+        const int h = token_hash(seqs + r * stride, len, t);
+        v = h < 0 ? 0 : h < kTokenHashes ? vocab[1 + h] : -1;
+    }
+    tokens[i] = v;
+}
+
+} // namespace
+
+int64_t encoder_tile_bytes() { return int64_t(kL) * kT * kYR * 2; }
+
+void encoder_upload(DeviceEncoder &d, const EncoderHost &h, int device)
+{
+    if ((int)h.emb_rows.size() != kRows * 64 || h.hidden != kH || h.emb_dim != 64 || h.max_len != kL)
+        throw Error(DRM_ERR_UNSUPPORTED, "encoder: unsupported model shape");
+    d.device = device;
+    d.h0 = h.h0;
+    DRM_HIP_CHECK(hipSetDevice(device));
+    auto up16 = [&](const std::vector<uint16_t> &v, uint16_t **p) {
+        DRM_HIP_CHECK(hipMalloc(p, v.size() * 2));
+        DRM_HIP_CHECK(hipMemcpy(*p, v.data(), v.size() * 2, hipMemcpyHostToDevice));
+        d.device_bytes += v.size() * 2;
+    };
+    up16(h.emb_rows, &d.emb);
+    up16(h.vocab_rows, &d.vocab);
+    for (int l = 0; l < 2; ++l) {
+        up16(h.W[l], &d.W[l]);
+        up16(h.R[l], &d.R[l]);
+        std::vector<float> b(h.B[l].size());
+        for (size_t i = 0; i < b.size(); ++i) {
+            _Float16 x;
+            memcpy(&x, &h.B[l][i], 2);
+            b[i] = (float)x;
+        }
+        DRM_HIP_CHECK(hipMalloc(&d.B[l], b.size() * 4));
+        DRM_HIP_CHECK(hipMemcpy(d.B[l], b.data(), b.size() * 4, hipMemcpyHostToDevice));
+    }
+    DRM_HIP_CHECK(hipMalloc(&d.flags, 16));
+    DRM_HIP_CHECK(hipMemset(d.flags, 0, 16));
+}
+
+void encoder_release(DeviceEncoder &d)
+{
+    (void)hipSetDevice(d.device);
+    for (void *p : {(void *)d.emb, (void *)d.vocab, (void *)d.W[0], (void *)d.W[1], (void *)d.R[0], (void *)d.R[1],
+                    (void *)d.B[0], (void *)d.B[1], (void *)d.y1, (void *)d.flags})
+        if (p) (void)hipFree(p);
+    d = DeviceEncoder{};
+}
+
+void launch_encode(DeviceEncoder &d, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
+                   float *d_out, hipStream_t stream)
+{
+    if (n <= 0) return;
+    const int64_t tiles = (n + kT - 1) / kT;
+    int64_t per = std::min<int64_t>(tiles, d.max_tiles_per_launch);
+    if (d.y1_tiles < per) {
+        if (d.y1) DRM_HIP_CHECK(hipFree(d.y1));
+        d.y1 = nullptr;
+        DRM_HIP_CHECK(hipMalloc(&d.y1, per * encoder_tile_bytes()));
+        d.y1_tiles = per;
+    }
+    EncArgs a{};
+    a.seqs = d_seqs;
+    a.lens = d_lens;
+    a.stride = stride;
+    a.n = n;
+    a.emb = (const _Float16 *)d.emb;
+    a.W1 = (const _Float16 *)d.W[0];
+    a.R1 = (const _Float16 *)d.R[0];
+    a.W2 = (const _Float16 *)d.W[1];
+    a.R2 = (const _Float16 *)d.R[1];
+    a.B1 = d.B[0];
+    a.B2 = d.B[1];
+    a.y1 = (_Float16 *)d.y1;
+    a.out = d_out;
+    a.h0 = d.h0;
+    a.flags = d.flags;
+    for (int64_t t0 = 0; t0 < tiles; t0 += per) {
+        a.first_tile = t0;
+        const int64_t nt = std::min(per, tiles - t0);
+        hipLaunchKernelGGL(gru_encode_kernel, dim3((unsigned)nt), dim3(512), 0, stream, a);
+        DRM_HIP_CHECK(hipGetLastError());
+    }
+}
+
+void launch_tokenize(const DeviceEncoder &d, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
+                     int32_t *d_tokens, hipStream_t stream)
+{
+    if (n <= 0) return;
+    const int64_t total = n * kL;
+    hipLaunchKernelGGL(tokenize_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, d_seqs, d_lens,
+                       stride, n, d.vocab, d_tokens);
+    DRM_HIP_CHECK(hipGetLastError());
+}
+
+} // namespace drm

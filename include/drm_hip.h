@@ -307,6 +307,42 @@ int drm_embed_kmer3(const uint8_t *seqs, const int64_t *off, const int32_t *len,
 int drm_embed_kmer3_device(const uint8_t *d_rows, int64_t n, int32_t len, int64_t row_stride, int32_t dim,
                            uint64_t seed, float *d_out, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Read encoder: Vectorizer (src/inference/vectorize.cpp:4-141) =
+ * Preprocessor::preprocess tokens (src/inference/preprocess.cpp:20-42) + the OpenVINO GRU model
+ * (src/inference/fast_model.cpp:3-68, models/finetuned_sgn33-new-a-Apr6.xml) on the GPU.
+ * -------------------------------------------------------------------------------------------*/
+typedef struct drm_encoder drm_encoder;
+typedef struct {
+    int32_t hidden, emb_dim, max_len, out_dim; /* 64, 64, 123 (config.hpp:21), 128 (config.hpp:22) */
+    int32_t n_token_rows;                     /* 97: padding + the 96 _Tok2Index tokens */
+    int32_t device;
+    float h0;
+    int64_t device_bytes;
+} drm_encoder_info;
+
+/* model_path: the reference's IR (.xml; weights from the sibling .bin, as core.read_model does,
+ * fast_model.cpp:15) or a .drmenc file written by drm_encoder_export. DRM_ERR_UNSUPPORTED for any
+ * graph other than embedding -> 2 x bidirectional GRU(64, linear_before_reset) with f16 weights. */
+int drm_encoder_load(const char *model_path, int device, drm_encoder **out);
+int drm_encoder_export(const char *model_path, const char *out_path); /* host only */
+int drm_encoder_free(drm_encoder *enc);
+int drm_encoder_get_info(const drm_encoder *enc, drm_encoder_info *info);
+/* Preprocessor::preprocess + prepareBatch padding: tokens [n][max_len] model-input vocabulary ids
+ * (0 = padding; -1 where the reference's hashToken indexes past its 96-entry table, which is
+ * undefined behaviour there). seqs: n rows of `stride` bytes, lens[i] >= 2 (DRM_ERR_ARG otherwise). */
+int drm_tokenize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride, int32_t *tokens);
+/* Vectorizer::vectorize: out [n][128] f32. n_undefined (optional): tokens that hit the reference's
+ * undefined table read (encoded with the padding row). */
+int drm_vectorize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride, float *out,
+                  int64_t *n_undefined);
+/* device buffers + stream, asynchronous; lens must be >= 2 (shorter sequences encode as padding and
+ * are counted by drm_encoder_flags) */
+int drm_vectorize_device(drm_encoder *enc, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
+                         float *d_out, void *stream);
+/* counters accumulated by drm_vectorize_device since the last call (synchronises the device) */
+int drm_encoder_flags(drm_encoder *enc, int64_t *n_undefined, int64_t *n_short);
+
 #ifdef __cplusplus
 }
 #endif
