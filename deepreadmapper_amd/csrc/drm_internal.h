@@ -165,6 +165,12 @@ struct EncoderHost {
 };
 std::vector<uint16_t> token_vocab_rows();
 EncoderHost read_encoder(const std::string &path); // .xml (IR + sibling .bin) or .drmenc; throws Error
+// Model the CLIs embed sequences with: DRM_ENCODER=<.xml|.drmenc> ("kmer3" or empty: the 3-mer stand-in),
+// else the reference's Config::Inference::MODEL_PATH relative to the working directory when it exists
+// (includes/utils/config.hpp:18), else "" (stand-in).
+std::string encoder_model_path();
+// Vectorizer::vectorize on `device` for host sequences: out [n][128]
+void vectorize_host(const std::string &model, int device, const std::vector<std::string> &seqs, float *out);
 void write_encoder(const EncoderHost &e, const std::string &path);
 
 } // namespace drm

@@ -8,8 +8,10 @@
 //   linear_before_reset, sigmoid/tanh, clip 0; W/R/B f16 Consts through Convert) -> GRUSequence
 //   (input 128) -> final hidden states; h0 = a scalar Const broadcast (ConstantOfShape).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iostream>
 #include <map>
 #include <sstream>
 
@@ -262,6 +264,44 @@ std::vector<uint16_t> token_vocab_rows() {
             for (int z = 0; z < 4; ++z) v[1 + 32 + (x << 4) + (y << 2) + z] = uint16_t(base + 1 + z);
         }
     return v;
+}
+
+std::string encoder_model_path() {
+    if (const char *e = std::getenv("DRM_ENCODER")) {
+        std::string v(e);
+        return v == "kmer3" ? std::string() : v;
+    }
+    const char *ref_model = "models/finetuned_sgn33-new-a-Apr6.xml";
+    std::ifstream f(ref_model);
+    return f ? std::string(ref_model) : std::string();
+}
+
+void vectorize_host(const std::string &model, int device, const std::vector<std::string> &seqs, float *out) {
+    drm_encoder *enc = nullptr;
+    auto chk = [](int rc) {
+        if (rc != DRM_OK) throw Error(rc, drm_last_error());
+    };
+    chk(drm_encoder_load(model.c_str(), device, &enc));
+    try {
+        size_t stride = 2;
+        for (auto &q : seqs) stride = std::max(stride, q.size());
+        std::vector<uint8_t> buf(seqs.size() * stride, 0);
+        std::vector<int32_t> lens(seqs.size());
+        for (size_t i = 0; i < seqs.size(); ++i) {
+            memcpy(&buf[i * stride], seqs[i].data(), seqs[i].size());
+            lens[i] = (int32_t)seqs[i].size();
+        }
+        int64_t undef = 0;
+        chk(drm_vectorize(enc, buf.data(), lens.data(), (int64_t)seqs.size(), (int64_t)stride, out, &undef));
+        if (undef)
+            std::cerr << "[INFERENCE] warning: " << undef
+                      << " tokens hash past the 96-entry token table (undefined in the reference; encoded as padding)"
+                      << std::endl;
+    } catch (...) {
+        drm_encoder_free(enc);
+        throw;
+    }
+    chk(drm_encoder_free(enc));
 }
 
 EncoderHost read_encoder(const std::string &path) {

@@ -311,7 +311,7 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
 }
 
 #ifndef DRM_PQ_SPEC
-#define DRM_PQ_SPEC 1 // codes + visited words of the predicted next row loaded one hop ahead
+#define DRM_PQ_SPEC 0 // codes + visited words of the predicted next row loaded one hop ahead (measured slower)
 #endif
 
 #define DRM_FSTAMP(idx)                                                                                     \

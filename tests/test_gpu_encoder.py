@@ -134,3 +134,37 @@ def test_gpu_embeddings_map_reads_to_source_windows(enc):
     nn = ((eq[:, None, :].astype(np.float64) - er[None, :, :]) ** 2).sum(-1).argmin(1)
     mapped = M.max(1) >= 100
     assert (M[np.arange(len(reads)), nn] == M.max(1))[mapped].mean() >= 0.9
+
+
+def test_cli_with_gru_encoder(tmp_path, enc):
+    """bin/hnswpq_index + bin/pipeline with DRM_ENCODER: windows and reads embedded by the GRU on the GPU
+    (the reference's index.cpp:279-280 and main.cpp:249-268 path). The index's vectors decode to the
+    encoder's window embeddings (PQ codes equal the oracle's encoding of them), and the pipeline's
+    indices/distances equal the oracle's faiss search over those encoder embeddings of the reads."""
+    import subprocess
+    from deepreadmapper_amd.encoder import DEFAULT_MODEL
+    from conftest import read_fastq_tagged
+    from oracle import faiss_file, oracle as O
+    fna = os.path.join(GOLDEN, "ecoli_150.fna")
+    fq = os.path.join(GOLDEN, "test_data.fastq")
+    env = dict(os.environ, DRM_BUILD_THREADS="1", DRM_ENCODER=DEFAULT_MODEL)
+    r = subprocess.run([os.path.join(ROOT, "bin", "hnswpq_index"), fna, "g1", "150"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "embedded by the GRU model" in r.stdout
+    r = subprocess.run([os.path.join(ROOT, "bin", "pipeline"), "g1", fq, fna, "128", "128", "5", "out"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Inference (GRU model" in r.stdout
+    reads = read_fastq_tagged(fq)
+    q = enc.vectorize(reads)
+    fx = faiss_file.read(str(tmp_path / "g1" / "g1.index"))
+    Do, Io, _, _ = O.hnswpq_search(fx, q, 128, 128)
+    I = np.load(tmp_path / "out" / "indices.npy")
+    D = np.load(tmp_path / "out" / "distances.npy")
+    assert np.array_equal(I.astype(np.int64), Io) and np.array_equal(D, Do)
+    # reads land on their source windows through the whole GRU -> PQ -> HNSW -> SW path
+    M = np.load(os.path.join(GOLDEN, "sw_c1_matrix.npy"))
+    ids = np.load(tmp_path / "out" / "sw_ids.npy").astype(np.int64)
+    mapped = M.max(1) >= 100
+    assert (M[np.arange(len(reads)), ids[:, 0]] == M.max(1))[mapped].mean() >= 0.9

@@ -4,8 +4,9 @@
 // Writes <index_prefix>/config.txt (keys of :289-302, save_config) and
 // <index_prefix>/<index_prefix>.index (:212) in faiss IndexHNSWPQ format.
 // Sequence inputs are read as tagged windows (read_file(ref, ref_len, stride), :270) and embedded
-// with the deterministic 3-mer stand-in (OpenVINO is out of scope). Extra knobs via env:
-// DRM_BUILD_THREADS (default: all cores), DRM_BUILD_SEED (default 0).
+// by the GRU model on the GPU (DRM_ENCODER, or the reference's models/ path in the working directory,
+// :279-280) or else the deterministic 3-mer stand-in. Extra knobs via env: DRM_BUILD_THREADS (default:
+// all cores), DRM_BUILD_SEED (default 0), DRM_DEVICE (encoder GPU).
 #include <cstdlib>
 #include <cstring>
 #include <filesystem>
@@ -61,17 +62,24 @@ int main(int argc, char *argv[])
                 return 1;
             }
             n = seqs.size();
-            std::string all;
-            std::vector<int64_t> off(n);
-            std::vector<int32_t> len(n);
-            for (size_t i = 0; i < n; ++i) {
-                off[i] = (int64_t)all.size();
-                len[i] = (int32_t)seqs[i].size();
-                all += seqs[i];
-            }
             emb.resize(n * dim);
-            drm::embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)n, (int)dim,
-                             drm::kEmbedSeed, emb.data());
+            const std::string model = drm::encoder_model_path();
+            if (!model.empty()) { // Vectorizer on the GPU (index.cpp:279-280)
+                const int device = std::getenv("DRM_DEVICE") ? std::atoi(std::getenv("DRM_DEVICE")) : 0;
+                drm::vectorize_host(model, device, seqs, emb.data());
+                std::cout << "[BUILD INDEX] " << n << " windows embedded by the GRU model " << model << std::endl;
+            } else {
+                std::string all;
+                std::vector<int64_t> off(n);
+                std::vector<int32_t> len(n);
+                for (size_t i = 0; i < n; ++i) {
+                    off[i] = (int64_t)all.size();
+                    len[i] = (int32_t)seqs[i].size();
+                    all += seqs[i];
+                }
+                drm::embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)n, (int)dim,
+                                 drm::kEmbedSeed, emb.data());
+            }
         }
         std::cout << "[BUILD INDEX] " << n << " vectors of dimension " << dim << std::endl;
         std::unordered_map<std::string, drm::ConfigValue> config = {

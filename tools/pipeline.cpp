@@ -12,9 +12,11 @@
 // instead of the static window table); use_streaming writes <output_dir>/results.sam block by block
 // (write_sam_streaming) and, like the reference, skips the .npy outputs -- the reference streams only in
 // its dynamic branch, so static + streaming writes no result file there either.
-// Differences, all documented in DESIGN.md: sequence inputs are embedded with the deterministic
-// 3-mer stand-in (the OpenVINO model is out of scope), and the rerank is the north star's SW rerank
-// (the reference's main runs an L2 rerank with the OpenVINO model at this point, src/main.cpp:312-331).
+// Sequence inputs are embedded by the reference's GRU model on the GPU (drm_vectorize) when
+// DRM_ENCODER names it (.xml IR or .drmenc) or when the reference's models/ path exists in the working
+// directory (Config::Inference::MODEL_PATH); otherwise by the deterministic 3-mer stand-in. The rerank is
+// the north star's SW rerank (the reference's main runs an L2 rerank with the model at this point,
+// src/main.cpp:312-331).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -209,23 +211,34 @@ int main(int argc, char *argv[])
                   << info.device_bytes / (1 << 20) << " MiB on each of " << devices.size() << " device(s))"
                   << std::endl;
 
-        // ---- embedding (stand-in for the OpenVINO model), into pinned host memory
+        // ---- embedding (Vectorizer::vectorize, src/main.cpp:249-268), into pinned host memory: the GRU model
+        //      on the GPU (DRM_ENCODER or the reference's models/ path), else the deterministic 3-mer stand-in
         if (!is_npy)
             dim = (size_t)info.d;
         Pinned<float> x(nq * dim);
         if (!is_npy) {
             t0 = clk::now();
-            std::string all;
-            std::vector<int64_t> off(nq);
-            std::vector<int32_t> len(nq);
-            for (size_t i = 0; i < nq; ++i) {
-                off[i] = (int64_t)all.size();
-                len[i] = (int32_t)qseqs[i].size();
-                all += qseqs[i];
+            const std::string model = drm::encoder_model_path();
+            if (!model.empty()) {
+                if (dim != 128)
+                    throw drm::Error(DRM_ERR_ARG, "the GRU model emits 128-d embeddings; the index has d = " +
+                                                      std::to_string(dim));
+                drm::vectorize_host(model, device, qseqs, x.p);
+                std::cout << "[MAIN] Inference (GRU model " << model << ", GPU) time: " << ms_since(t0) << " ms"
+                          << std::endl;
+            } else {
+                std::string all;
+                std::vector<int64_t> off(nq);
+                std::vector<int32_t> len(nq);
+                for (size_t i = 0; i < nq; ++i) {
+                    off[i] = (int64_t)all.size();
+                    len[i] = (int32_t)qseqs[i].size();
+                    all += qseqs[i];
+                }
+                check(drm_embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)nq, (int32_t)dim,
+                                      drm::kEmbedSeed, x.p));
+                std::cout << "[MAIN] Inference (3-mer stand-in) time: " << ms_since(t0) << " ms" << std::endl;
             }
-            check(drm_embed_kmer3((const uint8_t *)all.data(), off.data(), len.data(), (int64_t)nq, (int32_t)dim,
-                                  drm::kEmbedSeed, x.p));
-            std::cout << "[MAIN] Inference (3-mer stand-in) time: " << ms_since(t0) << " ms" << std::endl;
         } else {
             std::memcpy(x.p, emb.data(), sizeof(float) * nq * dim);
         }

@@ -13,6 +13,6 @@ for f in deepreadmapper_amd/csrc/*.hip; do
 done
 wait
 $ROCM/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$NAME.so ab/$NAME.obj/*.o build/capi.o build/exec.o build/faiss_io.o \
-  build/formats.o build/builder.o build/embed.o build/hnswlib_io.o build/builder_flat.o -L$ROCM/lib -lamdhip64 -lrccl -lgomp \
+  build/formats.o build/builder.o build/embed.o build/hnswlib_io.o build/builder_flat.o build/encoder.o -L$ROCM/lib -lamdhip64 -lrccl -lgomp \
   -Wl,-soname,libdrm_hip.so
 echo ab/$NAME.so
