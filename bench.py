@@ -210,7 +210,7 @@ def prepare_c5(args, D, dev):
     g = synth.genome(C5_GENOME, seed=44)
     n_ref = 2 * (C5_GENOME - 149)
     refs_path = os.path.join(args.cache, "c5_refs_150.u8")
-    index_path = os.path.join(args.cache, "c5_M16_efc200_s1_gpu.index")
+    index_path = os.path.join(args.cache, "c5_M16_efc200_s1_gpu" + ("_gru" if args.embed == "gru" else "") + ".index")
     if D.rank == 0:
         t0 = time.time()
         if not os.path.exists(refs_path):
@@ -219,7 +219,7 @@ def prepare_c5(args, D, dev):
             log(f"[bench] C5 window table ({n_ref} windows) written in {time.time() - t0:.1f}s")
         if not os.path.exists(index_path):
             rows = np.memmap(refs_path, dtype=np.uint8, mode="r", shape=(n_ref, 150))
-            synth.build_index_gpu_from_rows(rows, index_path + ".tmp", device=dev, log=log)
+            synth.build_index_gpu_from_rows(rows, index_path + ".tmp", device=dev, log=log, embed=args.embed)
             os.replace(index_path + ".tmp", index_path)
             del rows
         log(f"[bench] C5 workload ready in {time.time() - t0:.1f}s")
@@ -228,11 +228,49 @@ def prepare_c5(args, D, dev):
     t0 = time.time()
     reads, truth = synth.simulate_reads_range(g, D.rank * Q, (D.rank + 1) * Q, seed=9)
     queries = synth.tag(reads)
-    q_emb = synth.embed(queries)
-    log(f"[bench] {Q} reads simulated + embedded in {time.time() - t0:.1f}s")
+    q_emb = synth.embed_gru(queries, dev) if args.embed == "gru" else synth.embed(queries)
+    log(f"[bench] {Q} reads simulated + embedded ({args.embed}) in {time.time() - t0:.1f}s")
     return {"Q": Q, "refs": refs, "index_path": index_path, "q_emb": q_emb, "queries": queries, "truth": truth,
             "desc": f"C5 per-GPU slice: synthetic 50M x 150 bp dense IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200, "
-                    f"GPU-built), replicated per GPU, {Q} reads per GPU, search + SW rerank, EF=128 K=128"}
+                    f"GPU-built over {EMBED_DESC[args.embed]} window embeddings), replicated per GPU, {Q} reads per "
+                    f"GPU, search + SW rerank, EF=128 K=128"}
+
+
+EMBED_DESC = {"kmer3": "3-mer stand-in", "gru": "GRU-model (the reference's OpenVINO IR, on the GPU)"}
+ENC_PEAK_TFLOPS = 2500.0  # MI355X dense f16 MFMA (MI355X_MICROARCH.md matrix-core table)
+
+
+def encoder_timing(d_q, Q, q_stride, dev, reps=3):
+    """The GRU read encoder (drm_vectorize_device, encoder_gru.hip) on this rank's tagged reads resident
+    in HBM: HIP-event time of one launch sequence, reads/s, and MFMA rate against the f16 dense peak.
+    MFMA work per read (the hi/lo split counted): 2 dirs x 123 steps x 3 gates x 64 units x 2 flop x
+    (K1 = 64 h_hi + 64 h_lo + 64 x) + (K2 = 128 h + 256 x)."""
+    from deepreadmapper_amd.encoder import Encoder
+    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream
+    enc = Encoder(device=dev)
+    d_l = DeviceBuffer.from_host(np.full(Q, q_stride, dtype=np.int32))
+    d_o = DeviceBuffer((Q, 128), np.float32)
+    st = Stream()
+    enc.vectorize_device(d_q, d_l, Q, q_stride, d_o, st)
+    st.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = Event(), Event()
+        a.record(st)
+        enc.vectorize_device(d_q, d_l, Q, q_stride, d_o, st)
+        b.record(st)
+        st.synchronize()
+        ts.append(a.elapsed_ms(b))
+    ms = float(np.mean(ts))
+    flop_read = 2 * 123 * 3 * 64 * 2 * ((64 + 64 + 64) + (128 + 256))
+    tflops = Q * flop_read / (ms * 1e-3) / 1e12
+    und, short = enc.flags()
+    enc.free()
+    return {"kernel": "gru_encode_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": ENC_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / ENC_PEAK_TFLOPS, 4)},
+            "flop_per_read": flop_read, "undefined_tokens": und + short,
+            "note": "Vectorizer::vectorize on the GPU; not inside `value` (the north star's path starts at embeddings)"}
 
 
 def host_path(ix, table, q_emb, queries, K, EF, flat):
@@ -378,7 +416,7 @@ def run_c4(args, D):
             "value": round(r["value"], 1), "unit": "reads/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(r["ms"], 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32 (PQ-ADC distances)",
-            "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
+            "data": f"synthetic (seeded genome/reads, {EMBED_DESC[args.embed]} embeddings; no network)",
             "config": {"workload": "C4: synthetic 20 Mbp genome, stride-4 sparse IndexHNSWPQ of "
                                    f"{info.ntotal} windows (M_pq=8 nbits=8 M_hnsw=16 EFC=200, GPU-built), search only",
                        "n_refs": int(info.ntotal), "queries_per_gpu": Q, "ef": args.ef, "k": args.k,
@@ -406,6 +444,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of oracle CPU work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the pinned-host drm_search_rerank timing")
+    ap.add_argument("--no-encoder", action="store_true", help="skip the GRU read-encoder timing")
+    ap.add_argument("--embed", choices=["kmer3", "gru"], default=None,
+                    help="embeddings of windows and reads: gru (default for c5: the reference's GRU model, run on the "
+                         "GPU by drm_vectorize) or kmer3 (the deterministic 3-mer stand-in; default for c3/c4)")
     ap.add_argument("--build-threads", type=int, default=0)
     ap.add_argument("--index", choices=["pq", "flat"], default="pq",
                     help="pq (default): faiss IndexHNSWPQ, the live pipeline's index (src/main.cpp:236-237); flat: "
@@ -418,6 +460,10 @@ def main():
     _claim_stdout()
 
     D = Dist()
+    if args.embed is None:
+        args.embed = "gru" if args.workload == "c5" else "kmer3"
+    if args.embed == "gru" and (args.workload != "c5" or args.index != "pq"):
+        raise SystemExit("--embed gru builds the C5 PQ index only")
     if args.workload == "c4":
         return run_c4(args, D)
     from deepreadmapper_amd import synth
@@ -531,17 +577,19 @@ def main():
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
     cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
-    prof_path, pmc = committed_pmc(search_kernel, args.workload + ("_flat" if flat else ""))
+    pkey = args.workload + ("_flat" if flat else "") + ("_gru" if args.embed == "gru" else "")
+    prof_path, pmc = committed_pmc(search_kernel, pkey)
     traffic = None
     if pmc and "hbm_bytes_est" in pmc:
         traffic = float(pmc["hbm_bytes_est"])
-    sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, args.workload)
+    sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, pkey)
     ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
     sw_gcups = cells / (sw_ms * 1e-3) / 1e9
     # VALU issue ceiling of the SW DP: 4 SIMD x 16 lanes per CU, 2 cells per packed lane-op
     sw_peak_gcups = ncu * 64 * CLOCK_HZ / SW_VALU_PER_CELL / 1e9
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
+    enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
@@ -564,7 +612,7 @@ def main():
             "dtype": ("fp32 (L2 distances)" if flat else "fp32 (PQ-ADC distances)") + (
                 " + int32 (SW DP, bit-profile u16 kernel)" if os.environ.get("DRM_SW_BITPROFILE") == "1" else
                 " + fp16 fixed-point SW DP (2^-10 units, exact for scores < 1024)"),
-            "data": "synthetic (seeded genome/reads, 3-mer stand-in embeddings; no network)",
+            "data": f"synthetic (seeded genome/reads, {EMBED_DESC[args.embed]} embeddings; no network)",
             "config": {"workload": workload, "n_refs": int(len(refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
             "roofline": {"bound": "hbm", "kernel": search_kernel, "achieved": round(achieved, 2),
@@ -586,6 +634,8 @@ def main():
             "cpu_baseline": cpu,
             "gather": gather,
             "host_path": host,
+            "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
+            if enc else None,
             "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),

@@ -141,28 +141,57 @@ def build_index(x, path, M_pq=8, nbits=8, M_hnsw=16, efc=200, sample_rate=0.5, n
 
 
 def build_index_gpu_from_rows(rows, path, M_pq=8, nbits=8, M_hnsw=16, efc=200, sample_rate=0.5, seed=0, device=0,
-                              log=None):
-    """GPU build (drm_build_hnswpq_device) over the stand-in embeddings of fixed-length rows (e.g. the
-    window table): the rows are embedded on the device (drm_embed_kmer3_device) and never leave it."""
+                              log=None, embed="kmer3"):
+    """GPU build (drm_build_hnswpq_device) over embeddings of fixed-length rows (e.g. the window table),
+    computed on the device and never leaving it: embed="kmer3" the stand-in (drm_embed_kmer3_device),
+    embed="gru" the reference's GRU model (drm_vectorize_device) on the tagged rows '<' + row + '>', as
+    hnswpq_index embeds its windows (src/hnswpq/index.cpp:270-280)."""
     from .device import DeviceBuffer, set_device, synchronize
     import time
-    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    rows = np.asarray(rows)
     n, L = rows.shape
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     set_device(device)
     t0 = time.time()
-    d_rows = DeviceBuffer.from_host(rows)
     d_x = DeviceBuffer((n, 128), np.float32)
-    check(lib().drm_embed_kmer3_device(d_rows.ptr, n, L, L, 128, C.c_uint64(EMBED_SEED), d_x.ptr, None))
-    d_rows.free()
+    if embed == "gru":
+        from .encoder import Encoder
+        enc = Encoder(device=device)
+        chunk = 1 << 21
+        tagged = np.empty((min(chunk, n), L + 2), dtype=np.uint8)
+        tagged[:, 0], tagged[:, -1] = ord("<"), ord(">")
+        d_t = DeviceBuffer(tagged.shape, np.uint8)
+        d_l = DeviceBuffer.from_host(np.full(len(tagged), L + 2, dtype=np.int32))
+        for lo in range(0, n, chunk):
+            m = min(chunk, n - lo)
+            tagged[:m, 1:-1] = rows[lo:lo + m]
+            check(lib().drm_memcpy_h2d(d_t.ptr, ptr(tagged), m * (L + 2)))  # ordered after the last launch
+            check(lib().drm_vectorize_device(enc.handle, d_t.ptr, d_l.ptr, m, L + 2, d_x.ptr + lo * 512, None))
+        synchronize()
+        d_t.free()
+        enc.free()
+    else:
+        d_rows = DeviceBuffer.from_host(np.ascontiguousarray(rows, dtype=np.uint8))
+        check(lib().drm_embed_kmer3_device(d_rows.ptr, n, L, L, 128, C.c_uint64(EMBED_SEED), d_x.ptr, None))
+        d_rows.free()
     if log:
-        log(f"[synth] embedded {n} rows on the GPU in {time.time() - t0:.1f}s")
+        log(f"[synth] embedded {n} rows ({embed}) on the GPU in {time.time() - t0:.1f}s")
     check(lib().drm_build_hnswpq_device(d_x.ptr, n, 128, M_pq, nbits, M_hnsw, efc, sample_rate, C.c_uint64(seed),
                                         device, str(path).encode()))
     synchronize()
     d_x.free()
     if log:
         log(f"[synth] GPU-built IndexHNSWPQ over {n} vectors in {time.time() - t0:.1f}s")
+
+
+def embed_gru(tagged, device=0):
+    """GRU embeddings [n, 128] f32 of tagged sequences (rows of a [n, L] u8 array) on the GPU."""
+    from .encoder import Encoder
+    enc = Encoder(device=device)
+    t = np.ascontiguousarray(tagged, dtype=np.uint8)
+    out = enc.vectorize((t, np.full(len(t), t.shape[1], dtype=np.int32)))
+    enc.free()
+    return out
 
 
 def build_flat_index(x, path, M=64, efc=128, nthreads=0, seed=0):
