@@ -4,8 +4,9 @@
 // linear_before_reset) -> concat(final fwd h, final bwd h) of layer 2, as the IR
 // models/finetuned_sgn33-new-a-Apr6.xml runs it under OpenVINO (src/inference/fast_model.cpp).
 //
-// One workgroup = one tile of 32 reads, 8 waves: waves 0-3 run the forward direction, 4-7 the
-// backward one, wave w owning hidden units [16(w&3), +16). Each recurrence step is a [32 x K] x [K x 16]
+// Two kernels per chunk of tiles (32 reads each): layer 1, then layer 2; one workgroup = one (tile,
+// direction), 4 waves, wave w owning hidden units [16w, +16), so 3 independent workgroups share a CU
+// and their barriers and gate math overlap each other's MFMA chains. Each recurrence step is a [32 x K] x [K x 16]
 // product per gate on the 16x16x32 f16 MFMA: the weights are f16 in the IR (exact B operands, held in
 // VGPRs for the whole layer); the f32 state h enters as two f16 terms hi = f16(h), lo = f16(h - hi)
 // (~22 significant bits, f32 accumulation), so the recurrence stays f32-grade at the f16 matrix rate.
@@ -36,9 +37,7 @@ constexpr int kXS = 264; // LDS row stride (halfs) of staged layer-1 outputs: 52
 constexpr int kYR = 256; // layer-1 output row in HBM: hi[fwd 64 | bwd 64] | lo[fwd 64 | bwd 64]
 constexpr int kRows = 1 + kTokenHashes;
 constexpr int kTokStride = 128;
-constexpr size_t kHbBytes = size_t(2) * 2 * 2 * kT * kHS * 2;  // [dir][buf][hi/lo] images
-constexpr size_t kXbBytes = size_t(2) * 2 * kT * kXS * 2;      // [dir][buf] staged inputs (layer 2)
-static_assert(kRows * kES * 2 <= 16384 && 16384 + kT * kTokStride <= kXbBytes, "layer-1 LDS carve");
+static_assert(kRows * kES * 2 <= 16384, "embedding rows fit their LDS slot");
 
 __device__ __forceinline__ int lower(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
@@ -110,24 +109,27 @@ __device__ __forceinline__ void gates(const f4 &z, const f4 &r, const f4 &gx, co
     }
 }
 
-__global__ __launch_bounds__(512) void gru_encode_kernel(EncArgs a)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kHbBytes + kXbBytes];
-    _Float16 *hb = (_Float16 *)smem;
-    uint8_t *xreg = smem + kHbBytes;
-    _Float16 *embs = (_Float16 *)xreg;
-    uint8_t *toks = xreg + 16384;
-    _Float16 *xb = (_Float16 *)xreg;
+// one h image = 32 rows of kHS halfs + 64 halfs of pad, so the hi and lo images of a buffer sit 32 banks
+// apart (the layer-1 row copy reads both in one ds_read_b128 lane group)
+constexpr int kImg = kT * kHS + 64;
+constexpr size_t kHbDirBytes = size_t(2) * 2 * kImg * 2; // [buf][hi/lo] images of one direction
+constexpr size_t kXbDirBytes = size_t(2) * kT * kXS * 2;     // [buf] staged layer-1 rows of one direction
 
+// Layer 1 of one direction (blockIdx.y) for one tile (blockIdx.x): input = the tokens' embedding rows.
+// 4 waves, wave w owning units [16w, +16); writes h_t (hi, lo) of every step to the tile's layer-1 rows.
+__global__ __launch_bounds__(256) void gru_layer1_kernel(EncArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kHbDirBytes + 16384 + kT * kTokStride];
+    _Float16 *hb = (_Float16 *)smem;
+    _Float16 *embs = (_Float16 *)(smem + kHbDirBytes);
+    uint8_t *toks = smem + kHbDirBytes + 16384;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int dir = wave >> 2, j = ((wave & 3) << 4) + (lane & 15), kq = lane >> 4, c16 = lane & 15;
-    const int dt = tid & 255; // thread index within the direction
+    const int dir = blockIdx.y, j = (wave << 4) + (lane & 15), kq = lane >> 4, c16 = lane & 15;
     const int64_t r0 = (a.first_tile + blockIdx.x) * kT;
     _Float16 *y1 = a.y1 + (int64_t)blockIdx.x * kL * kT * kYR;
-    auto himg = [&](int d, int buf, int hl) { return hb + ((d * 2 + buf) * 2 + hl) * kT * kHS; };
+    auto himg = [&](int buf, int hl) { return hb + (buf * 2 + hl) * kImg; };
 
-    // ---- tokens of the tile (row ids into the embedding rows) + embedding rows + h0 images
-    for (int i = tid; i < kT * kTokStride; i += 512) {
+    for (int i = tid; i < kT * kTokStride; i += 256) {
         const int row = i / kTokStride, t = i % kTokStride;
         const int64_t r = r0 + row;
         int v = 0;
@@ -135,168 +137,175 @@ __global__ __launch_bounds__(512) void gru_encode_kernel(EncArgs a)
             const int len = a.lens[r];
             if (len >= 2) {
                 const int h = token_hash(a.seqs + r * a.stride, len, t);
-                if (h >= kTokenHashes) atomicAdd(&a.flags[0], 1u);
+                if (dir == 0 && h >= kTokenHashes) atomicAdd(&a.flags[0], 1u);
                 v = (h >= 0 && h < kTokenHashes) ? h + 1 : 0;
-            } else if (t == 0) {
+            } else if (t == 0 && dir == 0) {
                 atomicAdd(&a.flags[1], 1u);
             }
         }
         toks[i] = (uint8_t)v;
     }
-    for (int i = tid; i < kRows * 8; i += 512)
+    for (int i = tid; i < kRows * 8; i += 256)
         *(h8 *)(embs + (i >> 3) * kES + (i & 7) * 8) = *(const h8 *)(a.emb + i * 8);
     const _Float16 h0hi = (_Float16)a.h0, h0lo = (_Float16)(a.h0 - (float)h0hi);
-    auto init_h = [&]() {
-        for (int i = tid; i < 2 * kT * kH; i += 512) {
-            const int d = i / (kT * kH), row = (i / kH) % kT, c = i % kH;
-            himg(d, 0, 0)[row * kHS + c] = h0hi;
-            himg(d, 0, 1)[row * kHS + c] = h0lo;
-        }
-    };
-    init_h();
-
+    for (int i = tid; i < kT * kH; i += 256) {
+        himg(0, 0)[(i / kH) * kHS + i % kH] = h0hi;
+        himg(0, 1)[(i / kH) * kHS + i % kH] = h0lo;
+    }
     float hp[2][4];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int q = 0; q < 4; ++q) hp[rb][q] = a.h0;
 
-    // ---------------------------------------------------------------- layer 1 (input = embedding)
-    {
-        const _Float16 *R = a.R1 + dir * 3 * kH * kH, *W = a.W1 + dir * 3 * kH * 64;
-        h8 rf[3][2], wf[3][2];
+    const _Float16 *R = a.R1 + dir * 3 * kH * kH, *W = a.W1 + dir * 3 * kH * 64;
+    h8 rf[3][2], wf[3][2];
 #pragma unroll
-        for (int g = 0; g < 3; ++g)
+    for (int g = 0; g < 3; ++g)
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
-                wf[g][c] = *(const h8 *)(W + (g * kH + j) * 64 + c * 32 + kq * 8);
-            }
-        const float *B = a.B1 + dir * 4 * kH;
-        const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
+        for (int c = 0; c < 2; ++c) {
+            rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
+            wf[g][c] = *(const h8 *)(W + (g * kH + j) * 64 + c * 32 + kq * 8);
+        }
+    const float *B = a.B1 + dir * 4 * kH;
+    const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
+    __syncthreads();
+    for (int s = 0; s < kL; ++s) {
+        const int t = dir ? kL - 1 - s : s, cur = s & 1;
+        const _Float16 *hh = himg(cur, 0), *hl = himg(cur, 1);
+        _Float16 *nh = himg(cur ^ 1, 0), *nl = himg(cur ^ 1, 1);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int ar = rb * 16 + c16;
+            const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
+            const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
+            const int tr = toks[ar * kTokStride + t];
+            const h8 ax0 = *(const h8 *)(embs + tr * kES + kq * 8), ax1 = *(const h8 *)(embs + tr * kES + 32 + kq * 8);
+            f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
+            z = mfma(ax0, wf[0][0], z);
+            r = mfma(ax0, wf[1][0], r);
+            gx = mfma(ax0, wf[2][0], gx);
+            gh = mfma(ah0, rf[2][0], gh);
+            z = mfma(ax1, wf[0][1], z);
+            r = mfma(ax1, wf[1][1], r);
+            gx = mfma(ax1, wf[2][1], gx);
+            gh = mfma(ah1, rf[2][1], gh);
+            z = mfma(ah0, rf[0][0], z);
+            r = mfma(ah0, rf[1][0], r);
+            gh = mfma(al0, rf[2][0], gh);
+            z = mfma(ah1, rf[0][1], z);
+            r = mfma(ah1, rf[1][1], r);
+            gh = mfma(al1, rf[2][1], gh);
+            z = mfma(al0, rf[0][0], z);
+            r = mfma(al0, rf[1][0], r);
+            z = mfma(al1, rf[0][1], z);
+            r = mfma(al1, rf[1][1], r);
+            gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
+        }
         __syncthreads();
-        for (int s = 0; s < kL; ++s) {
-            const int t = dir ? kL - 1 - s : s, cur = s & 1;
-            const _Float16 *hh = himg(dir, cur, 0), *hl = himg(dir, cur, 1);
-            _Float16 *nh = himg(dir, cur ^ 1, 0), *nl = himg(dir, cur ^ 1, 1);
+        // h_t (hi, lo) of this direction -> the tile's layer-1 row t: 32 rows x 2 x 128 B, 2 x 16 B per thread
 #pragma unroll
-            for (int rb = 0; rb < 2; ++rb) {
-                const int ar = rb * 16 + c16;
-                const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
-                const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
-                const int tr = toks[ar * kTokStride + t];
-                const h8 ax0 = *(const h8 *)(embs + tr * kES + kq * 8), ax1 = *(const h8 *)(embs + tr * kES + 32 + kq * 8);
-                f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
-                z = mfma(ax0, wf[0][0], z);
-                r = mfma(ax0, wf[1][0], r);
-                gx = mfma(ax0, wf[2][0], gx);
-                gh = mfma(ah0, rf[2][0], gh);
-                z = mfma(ax1, wf[0][1], z);
-                r = mfma(ax1, wf[1][1], r);
-                gx = mfma(ax1, wf[2][1], gx);
-                gh = mfma(ah1, rf[2][1], gh);
-                z = mfma(ah0, rf[0][0], z);
-                r = mfma(ah0, rf[1][0], r);
-                gh = mfma(al0, rf[2][0], gh);
-                z = mfma(ah1, rf[0][1], z);
-                r = mfma(ah1, rf[1][1], r);
-                gh = mfma(al1, rf[2][1], gh);
-                z = mfma(al0, rf[0][0], z);
-                r = mfma(al0, rf[1][0], r);
-                z = mfma(al1, rf[0][1], z);
-                r = mfma(al1, rf[1][1], r);
-                gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
-            }
-            __syncthreads();
-            // this direction's h_t (hi, lo) -> HBM row t of layer 1's output
-            for (int c = dt; c < kT * 16; c += 256) {
-                const int row = c >> 4, hlsel = (c >> 3) & 1, seg = c & 7;
-                *(h8 *)(y1 + ((int64_t)t * kT + row) * kYR + hlsel * 128 + dir * kH + seg * 8) =
-                    *(const h8 *)((hlsel ? nl : nh) + row * kHS + seg * 8);
-            }
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 4, hlsel = (c >> 3) & 1, seg = c & 7;
+            *(h8 *)(y1 + ((int64_t)t * kT + row) * kYR + hlsel * 128 + dir * kH + seg * 8) =
+                *(const h8 *)((hlsel ? nl : nh) + row * kHS + seg * 8);
         }
     }
-    __syncthreads(); // layer-1 outputs of both directions written (workgroup-scope fence + barrier)
+}
 
-    // ---------------------------------------------------------------- layer 2 (input = [fwd1 | bwd1])
-    {
-        const _Float16 *R = a.R2 + dir * 3 * kH * kH, *W = a.W2 + dir * 3 * kH * 2 * kH;
-        h8 rf[3][2], wf[3][4];
+// Layer 2 of one direction (blockIdx.y) for one tile: input = layer 1's [fwd | bwd] rows (hi/lo),
+// staged through LDS one step ahead; writes the final state to out[:, 64 dir ..].
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gru_layer2_kernel(EncArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kHbDirBytes + kXbDirBytes];
+    _Float16 *hb = (_Float16 *)smem;
+    _Float16 *xb = (_Float16 *)(smem + kHbDirBytes);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int dir = blockIdx.y, j = (wave << 4) + (lane & 15), kq = lane >> 4, c16 = lane & 15;
+    const int64_t r0 = (a.first_tile + blockIdx.x) * kT;
+    const _Float16 *y1 = a.y1 + (int64_t)blockIdx.x * kL * kT * kYR;
+    auto himg = [&](int buf, int hl) { return hb + (buf * 2 + hl) * kImg; };
+
+    const _Float16 *R = a.R2 + dir * 3 * kH * kH, *W = a.W2 + dir * 3 * kH * 2 * kH;
+    h8 rf[3][2], wf[3][4];
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
+    for (int g = 0; g < 3; ++g) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
+        for (int c = 0; c < 2; ++c) rf[g][c] = *(const h8 *)(R + (g * kH + j) * kH + c * 32 + kq * 8);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) wf[g][c] = *(const h8 *)(W + (g * kH + j) * 2 * kH + c * 32 + kq * 8);
-        }
-        const float *B = a.B2 + dir * 4 * kH;
-        const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) hp[rb][q] = a.h0;
-        // 32 rows x 512 B of layer-1 output per step and direction: 4 x 16 B per thread
-        h8 xr[4];
-        auto load_x = [&](int t) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = dt + 256 * i, row = c >> 5, seg = c & 31;
-                xr[i] = *(const h8 *)(y1 + ((int64_t)t * kT + row) * kYR + seg * 8);
-            }
-        };
-        auto store_x = [&](int buf) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = dt + 256 * i, row = c >> 5, seg = c & 31;
-                *(h8 *)(xb + (dir * 2 + buf) * kT * kXS + row * kXS + seg * 8) = xr[i];
-            }
-        };
-        init_h();
-        load_x(dir ? kL - 1 : 0);
-        store_x(0);
-        __syncthreads();
-        for (int s = 0; s < kL; ++s) {
-            const int cur = s & 1;
-            if (s + 1 < kL) load_x(dir ? kL - 2 - s : s + 1);
-            const _Float16 *hh = himg(dir, cur, 0), *hl = himg(dir, cur, 1);
-            _Float16 *nh = himg(dir, cur ^ 1, 0), *nl = himg(dir, cur ^ 1, 1);
-            const _Float16 *xs = xb + (dir * 2 + cur) * kT * kXS;
-#pragma unroll
-            for (int rb = 0; rb < 2; ++rb) {
-                const int ar = rb * 16 + c16;
-                const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
-                const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
-                f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const h8 xh = *(const h8 *)(xs + ar * kXS + c * 32 + kq * 8);
-                    const h8 xl = *(const h8 *)(xs + ar * kXS + 128 + c * 32 + kq * 8);
-                    z = mfma(xh, wf[0][c], z);
-                    r = mfma(xh, wf[1][c], r);
-                    gx = mfma(xh, wf[2][c], gx);
-                    z = mfma(xl, wf[0][c], z);
-                    r = mfma(xl, wf[1][c], r);
-                    gx = mfma(xl, wf[2][c], gx);
-                }
-                gh = mfma(ah0, rf[2][0], gh);
-                z = mfma(ah0, rf[0][0], z);
-                r = mfma(ah0, rf[1][0], r);
-                gh = mfma(ah1, rf[2][1], gh);
-                z = mfma(ah1, rf[0][1], z);
-                r = mfma(ah1, rf[1][1], r);
-                gh = mfma(al0, rf[2][0], gh);
-                z = mfma(al0, rf[0][0], z);
-                r = mfma(al0, rf[1][0], r);
-                gh = mfma(al1, rf[2][1], gh);
-                z = mfma(al1, rf[0][1], z);
-                r = mfma(al1, rf[1][1], r);
-                gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
-            }
-            if (s + 1 < kL) store_x(cur ^ 1);
-            __syncthreads();
-        }
+        for (int c = 0; c < 4; ++c) wf[g][c] = *(const h8 *)(W + (g * kH + j) * 2 * kH + c * 32 + kq * 8);
     }
-    // final states of layer 2: [fwd | bwd] (the IR's Gather_6/7/8 + Concat)
+    const float *B = a.B2 + dir * 4 * kH;
+    const float bz = B[j], br = B[kH + j], bxn = B[2 * kH + j], bhn = B[3 * kH + j];
+    float hp[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hp[rb][q] = a.h0;
+    const _Float16 h0hi = (_Float16)a.h0, h0lo = (_Float16)(a.h0 - (float)h0hi);
+    for (int i = tid; i < kT * kH; i += 256) {
+        himg(0, 0)[(i / kH) * kHS + i % kH] = h0hi;
+        himg(0, 1)[(i / kH) * kHS + i % kH] = h0lo;
+    }
+    // 32 rows x 512 B of layer-1 output per step: 4 x 16 B per thread
+    h8 xr[4];
+    auto load_x = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i, row = c >> 5, seg = c & 31;
+            xr[i] = *(const h8 *)(y1 + ((int64_t)t * kT + row) * kYR + seg * 8);
+        }
+    };
+    auto store_x = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i, row = c >> 5, seg = c & 31;
+            *(h8 *)(xb + buf * kT * kXS + row * kXS + seg * 8) = xr[i];
+        }
+    };
+    load_x(dir ? kL - 1 : 0);
+    store_x(0);
+    __syncthreads();
+    for (int s = 0; s < kL; ++s) {
+        const int cur = s & 1;
+        if (s + 1 < kL) load_x(dir ? kL - 2 - s : s + 1);
+        const _Float16 *hh = himg(cur, 0), *hl = himg(cur, 1);
+        _Float16 *nh = himg(cur ^ 1, 0), *nl = himg(cur ^ 1, 1);
+        const _Float16 *xs = xb + cur * kT * kXS;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int ar = rb * 16 + c16;
+            const h8 ah0 = *(const h8 *)(hh + ar * kHS + kq * 8), ah1 = *(const h8 *)(hh + ar * kHS + 32 + kq * 8);
+            const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
+            f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const h8 xh = *(const h8 *)(xs + ar * kXS + c * 32 + kq * 8);
+                const h8 xl = *(const h8 *)(xs + ar * kXS + 128 + c * 32 + kq * 8);
+                z = mfma(xh, wf[0][c], z);
+                r = mfma(xh, wf[1][c], r);
+                gx = mfma(xh, wf[2][c], gx);
+                z = mfma(xl, wf[0][c], z);
+                r = mfma(xl, wf[1][c], r);
+                gx = mfma(xl, wf[2][c], gx);
+            }
+            gh = mfma(ah0, rf[2][0], gh);
+            z = mfma(ah0, rf[0][0], z);
+            r = mfma(ah0, rf[1][0], r);
+            gh = mfma(ah1, rf[2][1], gh);
+            z = mfma(ah1, rf[0][1], z);
+            r = mfma(ah1, rf[1][1], r);
+            gh = mfma(al0, rf[2][0], gh);
+            z = mfma(al0, rf[0][0], z);
+            r = mfma(al0, rf[1][0], r);
+            gh = mfma(al1, rf[2][1], gh);
+            z = mfma(al1, rf[0][1], z);
+            r = mfma(al1, rf[1][1], r);
+            gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
+        }
+        if (s + 1 < kL) store_x(cur ^ 1);
+        __syncthreads();
+    }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -398,7 +407,9 @@ void launch_encode(DeviceEncoder &d, const uint8_t *d_seqs, const int32_t *d_len
     for (int64_t t0 = 0; t0 < tiles; t0 += per) {
         a.first_tile = t0;
         const int64_t nt = std::min(per, tiles - t0);
-        hipLaunchKernelGGL(gru_encode_kernel, dim3((unsigned)nt), dim3(512), 0, stream, a);
+        hipLaunchKernelGGL(gru_layer1_kernel, dim3((unsigned)nt, 2), dim3(256), 0, stream, a);
+        DRM_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(gru_layer2_kernel, dim3((unsigned)nt, 2), dim3(256), 0, stream, a);
         DRM_HIP_CHECK(hipGetLastError());
     }
 }
