@@ -135,20 +135,22 @@ struct Heap {
     // path is walked on the scalar unit over two ballots (which child each node takes, whether it
     // moves up) -- a few SALU cycles per level instead of a chain of cross-lane round trips -- while
     // the one ds_bpermute that fetches the moving values is already in flight.
-    __device__ __forceinline__ void pop128(int lane, const PathConst &pc)
+    // returns the new root (slot 0), wave-uniform
+    __device__ __forceinline__ uint64_t pop128(int lane, const PathConst &pc)
     {
         const uint64_t val = readlane64(L, 63);
         const bool takeL = lane == 63 || L > R;
         const int ch = takeL ? 2 * lane + 1 : 2 * lane + 2;
         const uint64_t chv = takeL ? L : R;
         const uint64_t up = bperm64(chv, ch & 63);
-        const uint64_t lm = ballot(takeL), mv = ballot(!(val > chv));
+        // ballots of single compares (a ballot of a compound condition costs two extra VALU to
+        // re-materialise the lane mask); lane 63 always takes its L (slot 127 has no sibling)
+        const uint64_t lm = ballot(L > R) | (1ull << 63), mv = ballot(!(val > chv));
 #if DRM_PQ_VPATH
         // node p is on the sift-down path (its chosen child moves up) iff p and all its ancestors have
         // mv set and every ancestor chose the child toward p: one test per lane against its constant
         // ancestor masks, instead of a 7-step scalar walk
-        const bool inW = (mv & pc.A) == pc.A && (lm & pc.Aup) == pc.Lreq;
-        const uint64_t W = ballot(inW);
+        const uint64_t W = ballot((mv & pc.A) == pc.A) & ballot((lm & pc.Aup) == pc.Lreq);
         uint32_t hole = 0;
         if (W) {
             const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
@@ -174,19 +176,21 @@ struct Heap {
         const uint64_t rootv = (W & 1ull) ? readlane64(chv, 0) : val;
         if (lane == 63)
             R = rootv;
+        return rootv;
     }
 
     // heap_push(128, val) right after pop128: val enters at slot 127 (lane 63 L); its ancestors are
     // slots 63, 31, 15, 7, 3, 1 (the L halves of lanes 31, 15, 7, 3, 1, 0) and the root (lane 63 R).
     // Every holder compares its own ancestor with val in place; chain index m = 7 - bitlen(lane + 1)
     // receives its father's value (m < h) or val (m == h), fetched by one ds_bpermute.
-    __device__ __forceinline__ void push128(uint64_t val, int lane)
+    // rootv: the root after the pop (pop128's return); returns the root after the push, wave-uniform
+    __device__ __forceinline__ uint64_t push128(uint64_t val, int lane, uint64_t rootv)
     {
         const bool holderL = lane == 63 || (lane < 32 && ((lane + 1) & lane) == 0); // slots 127, 63, ..., 1
-        const bool anc = lane == 63 || holderL;                                    // ancestors: lane 63 is the root
+        // ancestors of slot 127: the L halves of lanes 0, 1, 3, 7, 15, 31 and lane 63 (its R is the root)
+        constexpr uint64_t kAnc = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const uint64_t av = lane == 63 ? R : L;
-        const int h = __builtin_popcountll(ballot(anc && val > av));
-        const uint64_t rootv = readlane64(R, 63);
+        const int h = __builtin_popcountll(ballot(val > av) & kAnc);
         const uint64_t fl = bperm64(L, lane >> 1);
         const uint64_t srcv = lane == 0 ? rootv : fl;
         const int m = 7 - bitlen((uint32_t)lane + 1u);
@@ -194,6 +198,7 @@ struct Heap {
             L = m < h ? srcv : val;
         if (h == 7 && lane == 63)
             R = val;
+        return h == 7 ? val : rootv;
     }
 
     // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
@@ -340,6 +345,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
     const int ef = a.ef, k = a.k, deg0 = a.deg0;
     const PathConst pconst(lane);
+    const uint64_t deg0m = deg0 >= 64 ? ~0ull : ((1ull << deg0) - 1ull); // lanes holding a link slot
     const uint32_t kInfKey = ord32(INFINITY);
 
     for (;;) {
@@ -422,8 +428,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const bool pickR = lane != 63 ? cR <= cL : cR < cL;
             const uint32_t pk = pickR ? cR : cL;
             const uint32_t d0 = wave_min_u32(pk);
-            const uint64_t tiedm = ballot(pk == d0 && !(lane == 63 && pickR));
             const uint64_t rightm = ballot(pickR);
+            const uint64_t tiedm = ballot(pk == d0) & ~(rightm & (1ull << 63)); // lane 63's R is slot 0, lowest
             int wl = 63;
             bool wR = true;
             if (tiedm) {
@@ -452,9 +458,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const bool hit = v0 == pred;
             if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
-            const uint64_t negm = ballot(lane < deg0 && v1 < 0);
+            const uint64_t negm = ballot(v1 < 0) & deg0m;
             const int jmax = negm ? __builtin_ctzll(negm) : deg0;
             const bool act = lane < jmax;
+            const uint64_t actm = jmax >= 64 ? ~0ull : ((1ull << jmax) - 1ull);
             uint2 c8 = make_uint2(0u, 0u);
             uint32_t old = 0xFFFFFFFFu;
             const uint32_t bit = 1u << (v1 & 31);
@@ -477,7 +484,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (use_spec && fresh) // the test was a load: mark the fresh links (non-returning atomics)
                 __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             DRM_FSTAMP(3);
-            const uint64_t fm = ballot(fresh);
+            const uint64_t fm = a.check_dups ? ballot(fresh) : ballot((old & bit) == 0u) & actm;
             const int nf = __builtin_popcountll(fm);
             ndis0 += nf;
             // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
@@ -531,18 +538,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (lo32(root) != kPopLo)
                         --nvalid;
                     if (ef == 128) {
-                        hp.pop128(lane, pconst);
-                        hp.push128(val, lane);
+                        root = hp.push128(val, lane, hp.pop128(lane, pconst));
                     } else {
                         hp.pop(kc, lane);
                         hp.push(kc, val, lane);
+                        root = readlane64(hp.R, 63);
                     }
                 } else {
                     ++kc;
                     hp.push(kc, val, lane);
+                    root = readlane64(hp.R, 63);
                 }
                 ++nvalid;
-                root = readlane64(hp.R, 63);
                 accm |= 1ull << l;
             }
             if (LOGRES && accm) {
