@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
-SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false>"  # what C3/C4 (ef = k = 128, PQ8x8) launch (hnsw_pq_fast.hip)
+SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8) launch (hnsw_pq_fast.hip)
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<152>"
 SW_VALU_PER_CELL = 556 / 152 / 2  # static ISA count of the sw_score_f16_kernel<152> row loop: 556 VALU per 152 cell pairs

@@ -331,7 +331,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     } while (0)
 
 // LOGRES: k == ef (result set from the log); else k <= 64 (register result set).
-template <bool LOGRES, bool STAMPS>
+// FIX128: k = ef = efSearch = 128 and no repeated links (the pipeline's EF = K = 128 on a clean
+// index) as compile-time constants: fewer live SGPRs (no spills to VGPR lanes, no kernel-argument
+// reloads inside the hop loop) and no duplicate-link pass.
+template <bool LOGRES, bool STAMPS, bool FIX128>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -343,7 +346,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
-    const int ef = a.ef, k = a.k, deg0 = a.deg0;
+    const int ef = FIX128 ? 128 : a.ef, k = FIX128 ? 128 : a.k, deg0 = a.deg0;
+    const int ef_search = FIX128 ? 128 : a.efSearch;
+    const bool check_dups = FIX128 ? false : (a.check_dups != 0);
     const PathConst pconst(lane);
     const uint64_t deg0m = deg0 >= 64 ? ~0ull : ((1ull << deg0) - 1ull); // lanes holding a link slot
     const uint32_t kInfKey = ord32(INFINITY);
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             nvalid--;
             // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
             const int below = __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
-            if (below >= a.efSearch)
+            if (below >= ef_search)
                 break;
             DRM_FSTAMP(2);
 
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 old = vis_test_set(&vis[v1 >> 5], bit);
             }
             bool fresh = act && (old & bit) == 0u;
-            if (a.check_dups) { // a repeated id in one row: only its first occurrence is fresh
+            if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
                     const int32_t vj = __shfl(v1, j, 64);
                     if (j < lane && vj == v1)
@@ -484,18 +489,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (use_spec && fresh) // the test was a load: mark the fresh links (non-returning atomics)
                 __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             DRM_FSTAMP(3);
-            const uint64_t fm = a.check_dups ? ballot(fresh) : ballot((old & bit) == 0u) & actm;
+            const uint64_t fm = check_dups ? ballot(fresh) : ballot((old & bit) == 0u) & actm;
             const int nf = __builtin_popcountll(fm);
             ndis0 += nf;
             // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
             // on the fresh ones)
+            // all 8 LDS reads in flight before the first add (the adds stay in sub-quantizer order)
+            float lv[8];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                lv[m] = lut[m * 256 + ((c8.x >> (8 * m)) & 255u)];
+                lv[m + 4] = lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             float r = 0.0f;
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-                r = __fadd_rn(r, lut[m * 256 + ((c8.x >> (8 * m)) & 255u)]);
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                r = __fadd_rn(r, lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)]);
+            for (int m = 0; m < 8; ++m)
+                r = __fadd_rn(r, lv[m]);
             const uint32_t dk = fresh ? ord32(r) : 0xFFFFFFFFu;
             {
                 // prefetch the row of the likely next pop_min (smallest valid slot or fresh link)
@@ -647,16 +657,19 @@ bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream)
 {
     const bool logres = a.k == a.ef;
-    if (logres) {
+    const bool fix = logres && a.k == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
+    if (fix)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (logres) {
         if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false>), dim3(slots), dim3(64), lds, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false>), dim3(slots), dim3(64), lds, stream, a);
     } else {
         if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true, false>), dim3(slots), dim3(64), lds, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false>), dim3(slots), dim3(64), lds, stream, a);
     }
     DRM_HIP_CHECK(hipGetLastError());
 }
