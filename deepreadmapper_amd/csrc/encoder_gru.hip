@@ -117,7 +117,10 @@ constexpr size_t kXbDirBytes = size_t(2) * kT * kXS * 2;     // [buf] staged lay
 
 // Layer 1 of one direction (blockIdx.y) for one tile (blockIdx.x): input = the tokens' embedding rows.
 // 4 waves, wave w owning units [16w, +16); writes h_t (hi, lo) of every step to the tile's layer-1 rows.
-__global__ __launch_bounds__(256) void gru_layer1_kernel(EncArgs a)
+#ifndef DRM_ENC_L1_WAVES
+#define DRM_ENC_L1_WAVES 3 // waves per SIMD of layer 1 (its two row blocks' accumulators are live together)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DRM_ENC_L1_WAVES))) void gru_layer1_kernel(EncArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kHbDirBytes + 16384 + kT * kTokStride];
     _Float16 *hb = (_Float16 *)smem;
@@ -174,6 +177,9 @@ __global__ __launch_bounds__(256) void gru_layer1_kernel(EncArgs a)
         const int t = dir ? kL - 1 - s : s, cur = s & 1;
         const _Float16 *hh = himg(cur, 0), *hl = himg(cur, 1);
         _Float16 *nh = himg(cur ^ 1, 0), *nl = himg(cur ^ 1, 1);
+        // both row blocks' MFMA chains first, then both gate epilogues: the second block's MFMAs
+        // execute while the first block's gate math issues
+        f4 z[2], r[2], gx[2], gh[2];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             const int ar = rb * 16 + c16;
@@ -181,27 +187,32 @@ __global__ __launch_bounds__(256) void gru_layer1_kernel(EncArgs a)
             const h8 al0 = *(const h8 *)(hl + ar * kHS + kq * 8), al1 = *(const h8 *)(hl + ar * kHS + 32 + kq * 8);
             const int tr = toks[ar * kTokStride + t];
             const h8 ax0 = *(const h8 *)(embs + tr * kES + kq * 8), ax1 = *(const h8 *)(embs + tr * kES + 32 + kq * 8);
-            f4 z = {bz, bz, bz, bz}, r = {br, br, br, br}, gx = {bxn, bxn, bxn, bxn}, gh = {bhn, bhn, bhn, bhn};
-            z = mfma(ax0, wf[0][0], z);
-            r = mfma(ax0, wf[1][0], r);
-            gx = mfma(ax0, wf[2][0], gx);
-            gh = mfma(ah0, rf[2][0], gh);
-            z = mfma(ax1, wf[0][1], z);
-            r = mfma(ax1, wf[1][1], r);
-            gx = mfma(ax1, wf[2][1], gx);
-            gh = mfma(ah1, rf[2][1], gh);
-            z = mfma(ah0, rf[0][0], z);
-            r = mfma(ah0, rf[1][0], r);
-            gh = mfma(al0, rf[2][0], gh);
-            z = mfma(ah1, rf[0][1], z);
-            r = mfma(ah1, rf[1][1], r);
-            gh = mfma(al1, rf[2][1], gh);
-            z = mfma(al0, rf[0][0], z);
-            r = mfma(al0, rf[1][0], r);
-            z = mfma(al1, rf[0][1], z);
-            r = mfma(al1, rf[1][1], r);
-            gates(z, r, gx, gh, hp[rb], rb * 16 + kq * 4, j, nh, nl);
+            z[rb] = f4{bz, bz, bz, bz};
+            r[rb] = f4{br, br, br, br};
+            gx[rb] = f4{bxn, bxn, bxn, bxn};
+            gh[rb] = f4{bhn, bhn, bhn, bhn};
+            z[rb] = mfma(ax0, wf[0][0], z[rb]);
+            r[rb] = mfma(ax0, wf[1][0], r[rb]);
+            gx[rb] = mfma(ax0, wf[2][0], gx[rb]);
+            gh[rb] = mfma(ah0, rf[2][0], gh[rb]);
+            z[rb] = mfma(ax1, wf[0][1], z[rb]);
+            r[rb] = mfma(ax1, wf[1][1], r[rb]);
+            gx[rb] = mfma(ax1, wf[2][1], gx[rb]);
+            gh[rb] = mfma(ah1, rf[2][1], gh[rb]);
+            z[rb] = mfma(ah0, rf[0][0], z[rb]);
+            r[rb] = mfma(ah0, rf[1][0], r[rb]);
+            gh[rb] = mfma(al0, rf[2][0], gh[rb]);
+            z[rb] = mfma(ah1, rf[0][1], z[rb]);
+            r[rb] = mfma(ah1, rf[1][1], r[rb]);
+            gh[rb] = mfma(al1, rf[2][1], gh[rb]);
+            z[rb] = mfma(al0, rf[0][0], z[rb]);
+            r[rb] = mfma(al0, rf[1][0], r[rb]);
+            z[rb] = mfma(al1, rf[0][1], z[rb]);
+            r[rb] = mfma(al1, rf[1][1], r[rb]);
         }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+            gates(z[rb], r[rb], gx[rb], gh[rb], hp[rb], rb * 16 + kq * 4, j, nh, nl);
         __syncthreads();
         // h_t (hi, lo) of this direction -> the tile's layer-1 row t: 32 rows x 2 x 128 B, 2 x 16 B per thread
 #pragma unroll
