@@ -1,0 +1,54 @@
+"""C5 at full size (BASELINE configs[4]): 50,000,000 stride-1 windows of a seeded
+25,000,149 bp genome, embedded by the GRU model and indexed on the GPU (the bench's default workload).
+A 512-read sample is checked bit-exactly against the oracle at this scale -- search ids, 0-ulp
+distances, ndis, nhops, SW scores and ids -- and the whole sample passes the size-independent checks
+(rows ascending, status == K). About two minutes on one MI355X, most of it building the workload."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C5_GENOME = 25_000_149
+SAMPLE = 512
+
+
+@pytest.fixture(scope="module")
+def c5(tmp_path_factory):
+    from deepreadmapper_amd import synth
+    d = tmp_path_factory.mktemp("c5")
+    g = synth.genome(C5_GENOME, seed=44)
+    refs = synth.windows_lookup(g, 150, 1)
+    assert refs.shape == (50_000_000, 150)
+    path = str(d / "c5_gru.index")
+    synth.build_index_gpu_from_rows(refs, path, embed="gru")
+    reads, truth = synth.simulate_reads_range(g, 0, SAMPLE, seed=9)
+    q = synth.tag(reads)
+    return {"refs": refs, "index": path, "q": q, "x": synth.embed_gru(q), "truth": truth}
+
+
+def test_c5_search_and_rerank_vs_oracle(c5):
+    from deepreadmapper_amd import read_index, WindowTable, rerank_arrays
+    from oracle import faiss_file, oracle as O
+    K = EF = 128
+    ix = read_index(c5["index"])
+    D, I, st = ix.search(c5["x"], K, EF)
+    fx = faiss_file.read(c5["index"])
+    Do, Io, nd, nh = O.hnswpq_search(fx, c5["x"], K, EF)
+    del fx
+    assert np.array_equal(I, Io)
+    assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))
+    assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+    assert (np.diff(D, axis=1) >= 0).all()
+    table = WindowTable(c5["refs"])
+    q = c5["q"]
+    ql = np.full(len(q), q.shape[1], dtype=np.int32)
+    sc, ids, cnt = rerank_arrays(table, I, (q, ql), 1, K, K)
+    rc, sco, ido, cnto = O.post_process_sw_static(I, c5["refs"], 150, q, ql, 1, K, K)
+    assert rc == 0 and (cnt == K).all()
+    assert np.array_equal(sc, sco) and np.array_equal(ids, ido)
+    # the GRU embeddings put most reads on their source window
+    assert float(np.mean(ids[:, 0].astype(np.int64) == c5["truth"])) > 0.6
+    table.free()
+    ix.free()
