@@ -337,7 +337,8 @@ int drm_tokenize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int
 int drm_vectorize(drm_encoder *enc, const uint8_t *seqs, const int32_t *lens, int64_t n, int64_t stride, float *out,
                   int64_t *n_undefined);
 /* device buffers + stream, asynchronous; lens must be >= 2 (shorter sequences encode as padding and
- * are counted by drm_encoder_flags) */
+ * are counted by drm_encoder_flags). Like the index handles, an encoder handle is single-stream: its
+ * layer-1 workspace is reused by every call, so calls must be serialised in stream order. */
 int drm_vectorize_device(drm_encoder *enc, const uint8_t *d_seqs, const int32_t *d_lens, int64_t n, int64_t stride,
                          float *d_out, void *stream);
 /* counters accumulated by drm_vectorize_device since the last call (synchronises the device) */
