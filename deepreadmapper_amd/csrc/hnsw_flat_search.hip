@@ -657,10 +657,26 @@ __device__ __forceinline__ void bitonic128(float (&k)[2], uint64_t (&l)[2])
 
 // NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
 // NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
-// MODE 0: the whole search (the only mode).
+// MODE 0: the whole search. MODE 1: the same with the common shape as compile-time constants
+// (d = 128, k = ef = 128, maxM0 = 128, maxM = 64, no repeated links, top heap fully in LDS): fewer
+// live SGPRs and no kernel-argument reloads in the hop loop.
 template <int NV, int NR, bool STAMPS, int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAVES))) void hnsw_flat_search_kernel(FlatArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAVES))) void hnsw_flat_search_kernel(FlatArgs a_in)
 {
+    FlatArgs a = a_in;
+    if (MODE == 1) {
+        a.d = 128;
+        a.k = 128;
+        a.ef = 128;
+        a.maxM0 = 128;
+        a.maxM = 64;
+        a.top_lds = 129;
+        a.top_ovf_cap = 0;
+        a.cand_lds = DRM_FLAT_CAND_LDS;
+        a.check_dups = 0;
+        a.qlist = nullptr;
+        a.qcount = nullptr;
+    }
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
     uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1231,7 +1247,13 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         else                                                                                                    \
             hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
     }
-    DRM_FLAT_MAIN(0)
+    const bool fixed = ix.d == 128 && k == 128 && efc == 128 && ix.maxM0 == 128 && ix.maxM == 64 && top_lds == 129 &&
+                       !ix.has_dup_links && !a.stamps && !a.qlist && DRM_FLAT_Q_REGS;
+    if (fixed)
+        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, false, 1>), dim3(slots), dim3(64), lds, stream, a);
+    else {
+        DRM_FLAT_MAIN(0)
+    }
 #undef DRM_FLAT_MAIN
     DRM_HIP_CHECK(hipGetLastError());
 }
