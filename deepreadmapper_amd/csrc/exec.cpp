@@ -87,7 +87,7 @@ struct Span {
 };
 struct BatchSet {
     Span x, q, ql, D, I, nd, nh, sc, id, st; // slices of the cache's one device arena
-    hipEvent_t in_done = nullptr, search_done = nullptr, comp_done = nullptr, out_done = nullptr;
+    hipEvent_t search_done = nullptr, comp_done = nullptr, out_done = nullptr;
     bool busy = false;
 };
 
@@ -97,7 +97,7 @@ constexpr int kSets = 3;
 // handle is single-stream, so one executor per handle never races), grown when a call needs more.
 struct ExecCache {
     int device = -1;
-    hipStream_t s_in = nullptr, s_search = nullptr, s_sw = nullptr, s_out = nullptr;
+    hipStream_t s_search = nullptr, s_sw = nullptr, s_out = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     BatchSet sets[kSets];
     int64_t B = 0, d = 0, kc = 0, kr = 0, q_stride = 0;
@@ -122,12 +122,12 @@ struct ExecCache {
     {
         device = dev;
         HC(hipSetDevice(dev));
-        for (hipStream_t *s : {&s_in, &s_search, &s_sw, &s_out})
+        for (hipStream_t *s : {&s_search, &s_sw, &s_out})
             HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         HC(hipEventCreate(&e0));
         HC(hipEventCreate(&e1));
         for (auto &b : sets)
-            for (hipEvent_t *e : {&b.in_done, &b.search_done, &b.comp_done, &b.out_done})
+            for (hipEvent_t *e : {&b.search_done, &b.comp_done, &b.out_done})
                 HC(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     void reserve(int64_t B_, int64_t d_, int64_t kc_, int64_t kr_, int64_t qs_, bool rr_)
@@ -163,7 +163,7 @@ struct ExecCache {
     }
     void drain()
     {
-        for (hipStream_t s : {s_in, s_search, s_sw, s_out})
+        for (hipStream_t s : {s_search, s_sw, s_out})
             if (s)
                 (void)hipStreamSynchronize(s);
         for (auto &b : sets)
@@ -176,13 +176,13 @@ struct ExecCache {
         (void)hipSetDevice(device);
         drain();
         for (auto &b : sets)
-            for (hipEvent_t e : {b.in_done, b.search_done, b.comp_done, b.out_done})
+            for (hipEvent_t e : {b.search_done, b.comp_done, b.out_done})
                 if (e)
                     (void)hipEventDestroy(e);
         for (hipEvent_t e : {e0, e1})
             if (e)
                 (void)hipEventDestroy(e);
-        for (hipStream_t s : {s_in, s_search, s_sw, s_out})
+        for (hipStream_t s : {s_search, s_sw, s_out})
             if (s)
                 (void)hipStreamDestroy(s);
         if (h_stats)
@@ -272,7 +272,8 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     };
     HC(hipSetDevice(info.device));
-    const int64_t B = std::min<int64_t>(n, batch_size_for(n));
+    const int64_t Bmax = std::min<int64_t>(n, batch_size_for(n));
+    const int64_t B = (n + (n + Bmax - 1) / Bmax - 1) / ((n + Bmax - 1) / Bmax); // equal batches, none tiny
     const size_t kc = (size_t)k_clusters, kr = rr ? (size_t)k : 0;
     ExecCache &ex = exec_for(index, info.device);
     try {
@@ -290,19 +291,19 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             s.busy = true;
             const int64_t nb = std::min(B, n - lo);
             const size_t m = (size_t)nb;
-            // host -> device (s_in)
-            HC(hipMemcpyAsync(s.x.p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_in));
+            // host -> device on the search stream: three streams, so that with HIP's default of four hardware
+            // queues per device (GPU_MAX_HW_QUEUES) none shares a queue; a copy stream sharing the rerank's queue
+            // serialised the copies behind the rerank kernels
+            HC(hipMemcpyAsync(s.x.p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_search));
             if (rr) {
                 HC(hipMemcpyAsync(s.q.p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice,
-                                  ex.s_in));
-                HC(hipMemcpyAsync(s.ql.p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_in));
+                                  ex.s_search));
+                HC(hipMemcpyAsync(s.ql.p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_search));
             }
-            HC(hipEventRecord(s.in_done, ex.s_in));
             if (verbose)
                 std::fprintf(stderr, "[exec]   b%lld copies in %.2f ms\n", (long long)b, ms_since());
-            // search (s_search), then rerank (s_sw): the next batch's search may start while this batch's
-            // rerank drains, filling the CUs its persistent grid leaves idle
-            HC(hipStreamWaitEvent(ex.s_search, s.in_done, 0));
+            // search (s_search, behind its input copies), then rerank (s_sw): the next batch's search may
+            // start while this batch's rerank drains, filling the CUs its persistent grid leaves idle
             abi_check(drm_search_device_ex(index, s.x.as<float>(), nb, k_clusters, ef, s.D.as<float>(),
                                            s.I.as<int64_t>(), s.nd.as<int32_t>(), s.nh.as<int32_t>(), nullptr,
                                            ex.s_search));
@@ -321,12 +322,14 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             HC(hipEventRecord(s.comp_done, s_last));
             if (verbose)
                 std::fprintf(stderr, "[exec]   b%lld rerank %.2f ms\n", (long long)b, ms_since());
-            // device -> host (s_out)
-            HC(hipStreamWaitEvent(ex.s_out, s.comp_done, 0));
+            // device -> host (s_out): the search results as soon as the search is done (their copy runs
+            // beside this batch's rerank), the rerank results after it
+            HC(hipStreamWaitEvent(ex.s_out, s.search_done, 0));
             HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D.p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
             HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I.p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
             HC(hipMemcpyAsync(nd_host + lo, s.nd.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
             HC(hipMemcpyAsync(nh_host + lo, s.nh.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
+            HC(hipStreamWaitEvent(ex.s_out, s.comp_done, 0));
             if (rr) {
                 HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc.p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
                                   ex.s_out));
@@ -408,9 +411,20 @@ int drm_search_rerank_prepare(drm_index *index, int64_t n, int32_t d, int32_t k_
         const bool rr = q_stride > 0;
         ex.reserve(std::min<int64_t>(n, batch_size_for(n)), d, k_clusters, rr ? k : 0, q_stride, rr);
         ex.reserve_stats(n);
-        // first use of the copy queues and the arena: a small round trip on both copy streams
-        HC(hipMemcpyAsync(ex.sets[0].nd.p, ex.h_stats, sizeof(int32_t), hipMemcpyHostToDevice, ex.s_in));
-        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].nd.p, sizeof(int32_t), hipMemcpyDeviceToHost, ex.s_out));
+        // first use of the copy queues and the arena: a round trip on both copy streams, large enough
+        // to take the DMA-engine path the batch copies take (a small copy goes another way)
+        const size_t wb = std::min(sizeof(int32_t) * 2 * (size_t)n, sizeof(float) * (size_t)ex.B * ex.kc);
+        HC(hipMemcpyAsync(ex.sets[0].D.p, ex.h_stats, wb, hipMemcpyHostToDevice, ex.s_search));
+        HC(hipStreamSynchronize(ex.s_search));
+        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].D.p, wb, hipMemcpyDeviceToHost, ex.s_out));
+        // first launch of the search kernel (code object load, scratch and the index's first touch): one
+        // small batch of zero queries whose results are dropped, so the first timed batch runs at speed
+        const int64_t nw = std::min<int64_t>(std::min<int64_t>(n, batch_size_for(n)), 1024);
+        BatchSet &s = ex.sets[0];
+        HC(hipMemsetAsync(s.x.p, 0, sizeof(float) * (size_t)nw * d, ex.s_search));
+        abi_check(drm_search_device_ex(index, s.x.as<float>(), nw, k_clusters, std::max(k_clusters, 16),
+                                       s.D.as<float>(), s.I.as<int64_t>(), s.nd.as<int32_t>(), s.nh.as<int32_t>(),
+                                       nullptr, ex.s_search));
         ex.drain();
     });
 }
