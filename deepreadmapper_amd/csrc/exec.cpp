@@ -97,7 +97,7 @@ constexpr int kSets = 3;
 // handle is single-stream, so one executor per handle never races), grown when a call needs more.
 struct ExecCache {
     int device = -1;
-    hipStream_t s_search = nullptr, s_sw = nullptr, s_out = nullptr;
+    hipStream_t s_search = nullptr, s_sw = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     BatchSet sets[kSets];
     int64_t B = 0, d = 0, kc = 0, kr = 0, q_stride = 0;
@@ -122,7 +122,7 @@ struct ExecCache {
     {
         device = dev;
         HC(hipSetDevice(dev));
-        for (hipStream_t *s : {&s_search, &s_sw, &s_out})
+        for (hipStream_t *s : {&s_search, &s_sw})
             HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         HC(hipEventCreate(&e0));
         HC(hipEventCreate(&e1));
@@ -163,7 +163,7 @@ struct ExecCache {
     }
     void drain()
     {
-        for (hipStream_t s : {s_search, s_sw, s_out})
+        for (hipStream_t s : {s_search, s_sw})
             if (s)
                 (void)hipStreamSynchronize(s);
         for (auto &b : sets)
@@ -182,7 +182,7 @@ struct ExecCache {
         for (hipEvent_t e : {e0, e1})
             if (e)
                 (void)hipEventDestroy(e);
-        for (hipStream_t s : {s_search, s_sw, s_out})
+        for (hipStream_t s : {s_search, s_sw})
             if (s)
                 (void)hipStreamDestroy(s);
         if (h_stats)
@@ -283,7 +283,33 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
         if (verbose)
             std::fprintf(stderr, "[exec] %lld queries, batch %lld: setup %.2f ms\n", (long long)n, (long long)B, ms_since());
         HC(hipEventRecord(ex.e0, ex.s_search));
-        int64_t b = 0;
+        // Two streams: s_search (uploads, search, downloads) and s_sw (rerank). HIP maps streams onto a few
+        // hardware queues per device (GPU_MAX_HW_QUEUES, 4 by default, the null stream and the caller's own
+        // streams included); two streams that land on one queue run in submission order, so a separate
+        // download stream that shared the rerank's queue put each batch's downloads between two reranks.
+        // With a rerank, a batch's search results are downloaded on s_search right after its search, and
+        // its rerank results one batch late, after the next search: the search stream waits for the
+        // rerank there, and has the slack for it (a search is shorter than a rerank). Without a rerank,
+        // s_sw is the download stream.
+        hipStream_t s_out = rr ? ex.s_search : ex.s_sw;
+        auto download_search = [&](BatchSet &s, int64_t lo, size_t m) {
+            HC(hipStreamWaitEvent(s_out, s.search_done, 0));
+            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D.p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, s_out));
+            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I.p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, s_out));
+            HC(hipMemcpyAsync(nd_host + lo, s.nd.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
+            HC(hipMemcpyAsync(nh_host + lo, s.nh.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
+        };
+        auto download_rerank = [&](BatchSet &s, int64_t lo, size_t m) {
+            HC(hipStreamWaitEvent(s_out, s.comp_done, 0));
+            HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc.p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
+                              s_out));
+            HC(hipMemcpyAsync(sw_ids + (size_t)lo * kr, s.id.p, sizeof(uint64_t) * m * kr, hipMemcpyDeviceToHost,
+                              s_out));
+            HC(hipMemcpyAsync(status + lo, s.st.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s_out));
+            HC(hipEventRecord(s.out_done, s_out));
+        };
+        int64_t b = 0, prev_lo = 0;
+        size_t prev_m = 0;
         for (int64_t lo = 0; lo < n; lo += B, ++b) {
             BatchSet &s = ex.sets[b % kSets];
             if (s.busy) // the set's previous batch has left the device
@@ -291,59 +317,43 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             s.busy = true;
             const int64_t nb = std::min(B, n - lo);
             const size_t m = (size_t)nb;
-            // host -> device on the search stream: three streams, so that with HIP's default of four hardware
-            // queues per device (GPU_MAX_HW_QUEUES) none shares a queue; a copy stream sharing the rerank's queue
-            // serialised the copies behind the rerank kernels
             HC(hipMemcpyAsync(s.x.p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_search));
             if (rr) {
                 HC(hipMemcpyAsync(s.q.p, queries + (size_t)lo * q_stride, m * q_stride, hipMemcpyHostToDevice,
                                   ex.s_search));
                 HC(hipMemcpyAsync(s.ql.p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_search));
             }
-            if (verbose)
-                std::fprintf(stderr, "[exec]   b%lld copies in %.2f ms\n", (long long)b, ms_since());
-            // search (s_search, behind its input copies), then rerank (s_sw): the next batch's search may
-            // start while this batch's rerank drains, filling the CUs its persistent grid leaves idle
+            // search (s_search, behind its uploads), then rerank (s_sw): the next batch's search runs while
+            // this batch's rerank drains
             abi_check(drm_search_device_ex(index, s.x.as<float>(), nb, k_clusters, ef, s.D.as<float>(),
                                            s.I.as<int64_t>(), s.nd.as<int32_t>(), s.nh.as<int32_t>(), nullptr,
                                            ex.s_search));
             HC(hipEventRecord(s.search_done, ex.s_search));
-            if (verbose)
-                std::fprintf(stderr, "[exec]   b%lld search %.2f ms\n", (long long)b, ms_since());
-            hipStream_t s_last = ex.s_search;
             if (rr) {
                 HC(hipStreamWaitEvent(ex.s_sw, s.search_done, 0));
                 auto *pp = genome_mode ? drm_post_process_sw_dynamic_device : drm_post_process_sw_static_device;
                 abi_check(pp(refs, s.I.as<int64_t>(), nb, k_clusters, s.q.as<uint8_t>(), s.ql.as<int32_t>(), q_stride,
                              stride, k, k_clusters, s.sc.as<int32_t>(), s.id.as<uint64_t>(), s.st.as<int32_t>(),
                              ex.s_sw));
-                s_last = ex.s_sw;
+                HC(hipEventRecord(s.comp_done, ex.s_sw));
+                download_search(s, lo, m);
+                if (b > 0)
+                    download_rerank(ex.sets[(b - 1) % kSets], prev_lo, prev_m);
+            } else {
+                download_search(s, lo, m);
+                HC(hipEventRecord(s.out_done, s_out));
             }
-            HC(hipEventRecord(s.comp_done, s_last));
-            if (verbose)
-                std::fprintf(stderr, "[exec]   b%lld rerank %.2f ms\n", (long long)b, ms_since());
-            // device -> host (s_out): the search results as soon as the search is done (their copy runs
-            // beside this batch's rerank), the rerank results after it
-            HC(hipStreamWaitEvent(ex.s_out, s.search_done, 0));
-            HC(hipMemcpyAsync(D + (size_t)lo * kc, s.D.p, sizeof(float) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(I + (size_t)lo * kc, s.I.p, sizeof(int64_t) * m * kc, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(nd_host + lo, s.nd.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipMemcpyAsync(nh_host + lo, s.nh.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
-            HC(hipStreamWaitEvent(ex.s_out, s.comp_done, 0));
-            if (rr) {
-                HC(hipMemcpyAsync(sw_scores + (size_t)lo * kr, s.sc.p, sizeof(int32_t) * m * kr, hipMemcpyDeviceToHost,
-                                  ex.s_out));
-                HC(hipMemcpyAsync(sw_ids + (size_t)lo * kr, s.id.p, sizeof(uint64_t) * m * kr, hipMemcpyDeviceToHost,
-                                  ex.s_out));
-                HC(hipMemcpyAsync(status + lo, s.st.p, sizeof(int32_t) * m, hipMemcpyDeviceToHost, ex.s_out));
-            }
-            HC(hipEventRecord(s.out_done, ex.s_out));
+            prev_lo = lo;
+            prev_m = m;
             if (verbose)
                 std::fprintf(stderr, "[exec] batch %lld enqueued %.2f ms\n", (long long)b, ms_since());
         }
+        // e1: the end of the last batch's compute (the device span excludes its download)
         HC(hipStreamWaitEvent(ex.s_search, ex.sets[(b - 1) % kSets].comp_done, 0));
         HC(hipEventRecord(ex.e1, ex.s_search));
-        HC(hipStreamSynchronize(ex.s_out));
+        if (rr)
+            download_rerank(ex.sets[(b - 1) % kSets], prev_lo, prev_m);
+        HC(hipStreamSynchronize(s_out));
         HC(hipEventSynchronize(ex.e1));
         ex.drain();
         float ms = 0.f;
@@ -411,12 +421,15 @@ int drm_search_rerank_prepare(drm_index *index, int64_t n, int32_t d, int32_t k_
         const bool rr = q_stride > 0;
         ex.reserve(std::min<int64_t>(n, batch_size_for(n)), d, k_clusters, rr ? k : 0, q_stride, rr);
         ex.reserve_stats(n);
-        // first use of the copy queues and the arena: a round trip on both copy streams, large enough
+        // first use of the copy engines and the arena: copies on both streams, large enough
         // to take the DMA-engine path the batch copies take (a small copy goes another way)
         const size_t wb = std::min(sizeof(int32_t) * 2 * (size_t)n, sizeof(float) * (size_t)ex.B * ex.kc);
         HC(hipMemcpyAsync(ex.sets[0].D.p, ex.h_stats, wb, hipMemcpyHostToDevice, ex.s_search));
         HC(hipStreamSynchronize(ex.s_search));
-        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].D.p, wb, hipMemcpyDeviceToHost, ex.s_out));
+        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].D.p, wb, hipMemcpyDeviceToHost, ex.s_search));
+        HC(hipStreamSynchronize(ex.s_search));
+        HC(hipMemcpyAsync(ex.h_stats, ex.sets[0].D.p, wb, hipMemcpyDeviceToHost, ex.s_sw));
+        HC(hipStreamSynchronize(ex.s_sw));
         // first launch of the search kernel (code object load, scratch and the index's first touch): one
         // small batch of zero queries whose results are dropped, so the first timed batch runs at speed
         const int64_t nw = std::min<int64_t>(std::min<int64_t>(n, batch_size_for(n)), 1024);
