@@ -202,7 +202,7 @@ int drm_host_free(void *ptr);
  * reference's faiss_search(index, emb, k_clusters, ef) followed by post_process_sw_static(neighbors,
  * distances, ref_seqs, query_seqs, ref_len, stride, k, k_clusters) (src/main.cpp:278, :333-341), run as
  * batches streamed through the device (host->device copies, kernels and device->host copies of
- * consecutive batches overlap on three streams; batch size DRM_BATCH, default 262144 queries).
+ * consecutive batches overlap on two streams; batch size DRM_BATCH, default 262144 queries).
  * Host pointers throughout:
  *   x [n x d] f32 -> D [n x k_clusters] f32, I [n x k_clusters] int64 (drm_search's outputs);
  *   refs == NULL: search only (queries ... status ignored); a genome handle (drm_refs_create_genome)
@@ -219,7 +219,8 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
                       drm_search_stats *stats);
 
 /* Optional: set up drm_search_rerank's streams and device buffers for a batch of n queries ahead of the
- * call (q_stride = 0: search only), so the call itself only streams data and runs kernels. */
+ * call (q_stride = 0: search only), and do the first-use work there (the copy engines' first DMA, the
+ * search kernel's first launch), so the call itself only streams data and runs kernels. */
 int drm_search_rerank_prepare(drm_index *index, int64_t n, int32_t d, int32_t k_clusters, int32_t k, int32_t q_stride);
 
 /* ---------------------------------------------------------------- multi-GPU fan-out
