@@ -547,6 +547,9 @@ def main():
     elapsed_max = D.allreduce(elapsed, "MAX")
     search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
     sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
+    if os.environ.get("DRM_BENCH_VERBOSE"):
+        print("per-step search ms", [round(e[0].elapsed_ms(e[1]), 2) for e in events],
+              "sw ms", [round(e[1].elapsed_ms(e[2]), 2) for e in events], file=sys.stderr, flush=True)
 
     # correctness / quality of this rank's last step
     if flat and ix.overflows():

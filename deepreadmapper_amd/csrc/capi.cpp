@@ -73,7 +73,7 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 {
     T *p = nullptr;
     size_t nb = sizeof(T) * std::max<size_t>(v.size(), 1);
-    DRM_HIP_CHECK(hipMalloc(&p, nb));
+    DRM_HIP_CHECK(drm::malloc_big((void **)&p, nb, drm::kBigIndex));
     if (!v.empty())
         DRM_HIP_CHECK(hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
     bytes += (int64_t)nb;
@@ -684,7 +684,7 @@ int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int6
         r->dev.ref_len = ref_len;
         r->dev.row_stride = std::max<int64_t>(16, ((int64_t)ref_len + 15) / 16 * 16);
         const size_t bytes = (size_t)std::max<int64_t>(n_ref, 1) * (size_t)r->dev.row_stride;
-        DRM_HIP_CHECK(hipMalloc(&r->dev.windows, bytes));
+        DRM_HIP_CHECK(drm::malloc_big((void **)&r->dev.windows, bytes, drm::kBigWindows));
         DRM_HIP_CHECK(hipMemset(r->dev.windows, 0, bytes));
         if (n_ref > 0 && ref_len > 0) {
             // pageable host rows of ref_len bytes: a 2D host-to-device copy of tens of millions of short
@@ -721,7 +721,7 @@ int drm_refs_create_genome(const uint8_t *genome, int64_t len, int32_t ref_len, 
         r->dev.row_stride = 16;
         r->dev.glen = len;
         r->dev.n_ref = len >= ref_len ? 2 * (len - ref_len + 1) : 0;
-        DRM_HIP_CHECK(hipMalloc(&r->dev.genome, (size_t)std::max<int64_t>(len, 1)));
+        DRM_HIP_CHECK(drm::malloc_big((void **)&r->dev.genome, (size_t)std::max<int64_t>(len, 1), drm::kBigWindows));
         if (len > 0)
             DRM_HIP_CHECK(hipMemcpy(r->dev.genome, genome, (size_t)len, hipMemcpyHostToDevice));
         *out = r.release();

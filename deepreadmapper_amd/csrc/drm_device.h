@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "drm_internal.h"
@@ -16,6 +18,28 @@
     } while (0)
 
 namespace drm {
+
+// Large, randomly accessed device arrays (index rows and codes, visited bitmaps, window table). With
+// DRM_CONTIG (a mask of the kinds below) they are asked for as physically contiguous memory; plain
+// hipMalloc otherwise, or when the driver cannot. Measured: contiguous placement makes the C5 search
+// slower, so the default mask is 0.
+enum BigKind { kBigIndex = 1, kBigVisited = 2, kBigWindows = 4 };
+inline hipError_t malloc_big(void **p, size_t bytes, BigKind kind)
+{
+    static const int mask = [] {
+        const char *e = std::getenv("DRM_CONTIG");
+        return e ? std::atoi(e) : 0;
+    }();
+    if ((mask & (int)kind) && bytes >= ((size_t)64 << 20)) {
+        const hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+        if (std::getenv("DRM_CONTIG_LOG"))
+            std::fprintf(stderr, "[contig] %zu MiB: %s\n", bytes >> 20, e == hipSuccess ? "contiguous" : "fallback");
+        if (e == hipSuccess)
+            return hipSuccess;
+        (void)hipGetLastError();
+    }
+    return hipMalloc(p, bytes);
+}
 
 constexpr int kMaxLevels = 24; // HNSW levels representable in SearchArgs::cum
 

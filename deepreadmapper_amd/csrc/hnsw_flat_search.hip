@@ -1147,7 +1147,7 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
         ix.vis_words = std::max<int64_t>(words, 1);
         ix.clear_cap = 16384;
         ix.cand_ovf_cap = ovf_cap;
-        DRM_HIP_CHECK(hipMalloc(&ix.visited, sizeof(uint32_t) * (size_t)alloc * (size_t)ix.vis_words));
+        DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)alloc * (size_t)ix.vis_words, kBigVisited));
         DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)alloc * (size_t)ix.vis_words));
         DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)alloc * (size_t)ix.clear_cap));
         DRM_HIP_CHECK(hipMalloc(&ix.cand_ovf_k, sizeof(float) * (size_t)alloc * (size_t)ovf_cap));

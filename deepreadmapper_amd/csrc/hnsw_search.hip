@@ -1024,7 +1024,7 @@ void reserve_search_scratch(DeviceIndex &ix)
     const int slots = cus * per_cu;
     ix.vis_words = std::max<int64_t>((ix.ntotal + 31) / 32, 1);
     ix.clear_cap = 16384;
-    DRM_HIP_CHECK(hipMalloc(&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
+    DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words, kBigVisited));
     DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
     DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)slots * (size_t)ix.clear_cap));
     ix.n_slots = slots;
@@ -1083,7 +1083,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
         const int alloc_slots = std::max(slots, (int)std::min<int64_t>((int64_t)cus * per_cu, 1 << 20));
         ix.vis_words = std::max<int64_t>(words, 1);
         ix.clear_cap = 16384;
-        DRM_HIP_CHECK(hipMalloc(&ix.visited, sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words));
+        DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words, kBigVisited));
         DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words));
         DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)alloc_slots * (size_t)ix.clear_cap));
         ix.n_slots = alloc_slots;
