@@ -15,7 +15,7 @@ HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -ffp-contract=off -munsafe-fp-atomi
 HOSTFLAGS := $(COMMON) -fopenmp -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
 LIB := $(PKG)/libdrm_hip.so
-HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/hnsw_pq_fast.o $(BUILD)/builder_gpu.o $(BUILD)/embed_gpu.o $(BUILD)/hnsw_search_lds.o $(BUILD)/hnsw_flat_search.o $(BUILD)/sw_rerank.o \
+HIP_OBJS := $(BUILD)/hnsw_search.o $(BUILD)/hnsw_pq_fast.o $(BUILD)/builder_gpu.o $(BUILD)/embed_gpu.o $(BUILD)/hnsw_search_lds.o $(BUILD)/hnsw_flat_search.o $(BUILD)/sw_rerank.o $(BUILD)/l2_rerank.o \
             $(BUILD)/encoder_gru.o $(BUILD)/capi.o $(BUILD)/exec.o
 HOST_OBJS := $(BUILD)/faiss_io.o $(BUILD)/formats.o $(BUILD)/builder.o $(BUILD)/embed.o $(BUILD)/hnswlib_io.o \
              $(BUILD)/builder_flat.o $(BUILD)/encoder.o

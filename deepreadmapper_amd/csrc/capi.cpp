@@ -758,7 +758,7 @@ int drm_refs_free(drm_refs *refs)
             return;
         (void)hipSetDevice(refs->dev.device);
         for (void *p : {(void *)refs->dev.windows, (void *)refs->dev.ws_ids, (void *)refs->dev.ws_scores,
-                        (void *)refs->dev.ws_ncand, (void *)refs->dev.genome})
+                        (void *)refs->dev.ws_ncand, (void *)refs->dev.genome, (void *)refs->dev.emb})
             if (p)
                 (void)hipFree(p);
         delete refs;
@@ -940,6 +940,148 @@ int drm_post_process_sw_dynamic(drm_refs *refs, const int64_t *neighbors, int64_
 {
     return post_process_host(true, refs, neighbors, nq, kk, queries, q_len, q_stride, stride, k, k_clusters,
                              top_scores, top_ids, counts, bad_query);
+}
+
+// ------------------------------------------------------------------------------- L2 rerank
+static drm::L2Args make_l2_args(drm_refs *refs, const int64_t *nb, int64_t nq, int32_t kk, const float *qe, int32_t d,
+                                int64_t stride, int32_t k_clusters, float *td, uint64_t *ti, int32_t *st)
+{
+    require_mode(refs, false);
+    if (!refs->dev.emb)
+        throw Error(DRM_ERR_ARG, "the window table has no embeddings: call drm_refs_embed first");
+    if (d != refs->dev.emb_dim)
+        throw Error(DRM_ERR_ARG, "Vector sizes mismatch: " + std::to_string(refs->dev.emb_dim) + " vs " +
+                                     std::to_string(d)); // calc_l2_dist, metrics.cpp:50-53
+    if (stride < 1)
+        throw Error(DRM_ERR_ARG, "stride must be >= 1");
+    if (nq < 0 || kk < 0 || k_clusters < 0)
+        throw Error(DRM_ERR_ARG, "negative nq / kk / k_clusters");
+    drm::L2Args a{};
+    a.emb = refs->dev.emb;
+    a.n_ref = refs->dev.n_ref;
+    a.d = d;
+    a.neighbors = nb;
+    a.kk = kk;
+    a.stride = stride;
+    a.query_emb = qe;
+    a.k = k_clusters;
+    a.nq = nq;
+    a.top_dists = td;
+    a.top_ids = ti;
+    a.status = st;
+    return a;
+}
+
+int drm_refs_embed(drm_refs *refs, drm_encoder *enc, void *stream)
+{
+    return guarded([&] {
+        if (!refs || !enc)
+            throw Error(DRM_ERR_ARG, "null argument");
+        require_mode(refs, false);
+        if (refs->dev.device != enc->dev.device)
+            throw Error(DRM_ERR_ARG, "window table and encoder live on different devices");
+        if (refs->dev.ref_len < 2)
+            throw Error(DRM_ERR_ARG, "windows shorter than 2 bytes cannot be vectorized");
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        hipStream_t s = (hipStream_t)stream;
+        const int64_t n = refs->dev.n_ref, d = 128;
+        if (!refs->dev.emb)
+            DRM_HIP_CHECK(drm::malloc_big((void **)&refs->dev.emb, sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d,
+                                          drm::kBigWindows));
+        refs->dev.emb_dim = (int32_t)d;
+        const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), (int64_t)4 << 20);
+        DevBuf<int32_t> lens((size_t)chunk);
+        {
+            std::vector<int32_t> h((size_t)chunk, refs->dev.ref_len);
+            lens.upload(h.data());
+        }
+        for (int64_t r0 = 0; r0 < n; r0 += chunk)
+            drm::launch_encode(enc->dev, refs->dev.windows + r0 * refs->dev.row_stride, lens.p,
+                               std::min(chunk, n - r0), refs->dev.row_stride, refs->dev.emb + r0 * d, s);
+        DRM_HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int drm_refs_embeddings(drm_refs *refs, const float **d_emb, int32_t *dim)
+{
+    return guarded([&] {
+        if (!refs || !d_emb)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *d_emb = refs->dev.emb;
+        if (dim)
+            *dim = refs->dev.emb_dim;
+    });
+}
+
+int drm_post_process_l2_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const float *d_query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                                      float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream)
+{
+    return guarded([&] {
+        drm::L2Args a = make_l2_args(refs, d_neighbors, nq, kk, d_query_emb, d, stride, k_clusters, d_top_dists,
+                                     d_top_ids, d_status);
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        drm::launch_l2_rerank(refs->dev, a, (hipStream_t)stream);
+    });
+}
+
+int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const float *query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                               float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query)
+{
+    return guarded([&] {
+        drm::L2Args a = make_l2_args(refs, nullptr, nq, kk, nullptr, d, stride, k_clusters, nullptr, nullptr, nullptr);
+        if (bad_query)
+            *bad_query = -1;
+        if (nq <= 0)
+            return;
+        if (!neighbors || !query_emb || !top_dists || !top_ids || !counts)
+            throw Error(DRM_ERR_ARG, "null argument");
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        DevBuf<int64_t> dn((size_t)nq * kk);
+        DevBuf<float> dqe((size_t)nq * d), dd((size_t)nq * k_clusters);
+        DevBuf<int32_t> dst((size_t)nq);
+        DevBuf<uint64_t> di((size_t)nq * k_clusters);
+        if (dn.n)
+            dn.upload(neighbors);
+        dqe.upload(query_emb);
+        a.neighbors = dn.p;
+        a.query_emb = dqe.p;
+        a.top_dists = dd.p;
+        a.top_ids = di.p;
+        a.status = dst.p;
+        drm::launch_l2_rerank(refs->dev, a, nullptr);
+        DRM_HIP_CHECK(hipDeviceSynchronize());
+        std::vector<int32_t> st((size_t)nq);
+        dst.download(st.data());
+        if (dd.n) {
+            dd.download(top_dists);
+            di.download(top_ids);
+        }
+        int64_t first_bad = -1, first_ids = -1;
+        for (int64_t i = 0; i < nq; ++i) {
+            counts[i] = st[(size_t)i] > 0 ? st[(size_t)i] : 0;
+            if (st[(size_t)i] == -1 && first_bad < 0)
+                first_bad = i;
+            if (st[(size_t)i] == -4 && first_ids < 0)
+                first_ids = i;
+        }
+        if (first_ids >= 0) {
+            if (bad_query)
+                *bad_query = first_ids;
+            throw Error(DRM_ERR_ARG, "Invalid mapping index in expansion (query " + std::to_string(first_ids) +
+                                         ": a label outside the window table, or a candidate range past the "
+                                         "expanded stream)"); // post_processor.cpp:1100-1106
+        }
+        if (first_bad >= 0) {
+            if (bad_query)
+                *bad_query = first_bad;
+            const int64_t nc = stride == 1 ? (int64_t)kk : (int64_t)kk * stride;
+            throw Error(DRM_ERR_CANDS, "Not enough candidates (" + std::to_string(nc) + " < " +
+                                           std::to_string(k_clusters) + ") for query " +
+                                           std::to_string(first_bad)); // reranker.cpp:154-158
+        }
+    });
 }
 
 } // extern "C"

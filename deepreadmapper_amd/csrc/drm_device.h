@@ -223,6 +223,10 @@ struct DeviceRefs {
     // table; window id w is genome[w / 2 ..+ ref_len), reverse-complemented when w is odd
     uint8_t *genome = nullptr;
     int64_t glen = 0;
+    // L2 rerank (post_process_l2_static): the read encoder's embedding of every window,
+    // [n_ref][emb_dim] f32, filled once by drm_refs_embed (l2_rerank.hip)
+    float *emb = nullptr;
+    int32_t emb_dim = 0;
 };
 
 struct RerankArgs {
@@ -259,6 +263,24 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
 void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *d_len1, const uint8_t *d_s2,
                      const int64_t *d_off2, const int32_t *d_len2, int64_t npairs, int32_t *d_scores, int max_len2,
                      hipStream_t stream);
+
+// L2 rerank (post_process_l2_static -> batch_reranker, src/utils/post_processor.cpp:1023-1162,
+// src/utils/reranker.cpp:98-195): distances from the window embedding table, libstdc++ partial_sort
+struct L2Args {
+    const float *emb;          // [n_ref][d] window embeddings
+    int64_t n_ref;
+    int32_t d;
+    const int64_t *neighbors;  // [nq][kk]
+    int32_t kk;
+    int64_t stride;
+    const float *query_emb;    // [nq][d]
+    int32_t k;                 // rows kept per query (batch_reranker's k = k_clusters)
+    int64_t nq;
+    float *top_dists;          // [nq][k]
+    uint64_t *top_ids;         // [nq][k]
+    int32_t *status;           // [nq]
+};
+void launch_l2_rerank(DeviceRefs &refs, L2Args a, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------- read encoder
 // HBM image of the GRU read encoder (encoder_gru.hip)

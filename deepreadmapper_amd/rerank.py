@@ -232,3 +232,59 @@ def partial_sort_order(scores, k):
     _, ids, _ = rerank_arrays(table, nb, [q], 1, k, n)
     table.free()
     return [int(i) for i in ids[0]]
+
+
+# ------------------------------------------------------------------------------------------- L2 rerank
+def embed_windows(table, encoder, stream=None):
+    """Fill the table's device embedding of every window with the read encoder (drm_refs_embed): the rows the
+    reference's post_process_l2_static re-embeds per run (src/utils/post_processor.cpp:1075-1080)."""
+    check(lib().drm_refs_embed(table.handle, encoder.handle, stream.handle if stream is not None else None))
+
+
+def window_embeddings_ptr(table):
+    """(device pointer, width) of the table's window embeddings (0, 0 before embed_windows)."""
+    p, d = C.c_void_p(), C.c_int32(0)
+    check(lib().drm_refs_embeddings(table.handle, C.byref(p), C.byref(d)))
+    return p.value or 0, d.value
+
+
+def l2_rerank_arrays(table, neighbors, query_embeddings, stride, k_clusters):
+    """Array form of post_process_l2_static on an embedded WindowTable: (dists [nq,k_clusters] f32,
+    ids [nq,k_clusters] u64, counts [nq])."""
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    nq, kk = nb.shape
+    qe = np.ascontiguousarray(query_embeddings, dtype=np.float32)
+    if qe.shape[0] != nq:
+        raise ValueError("one query embedding per neighbor row")
+    dists = np.empty((nq, k_clusters), dtype=np.float32)
+    ids = np.empty((nq, k_clusters), dtype=np.uint64)
+    counts = np.empty(nq, dtype=np.int32)
+    bad = C.c_int64(-1)
+    check(lib().drm_post_process_l2_static(table.handle, ptr(nb), nq, kk, ptr(qe), qe.shape[1], int(stride),
+                                           int(k_clusters), ptr(dists), ptr(ids), ptr(counts), C.byref(bad)))
+    return dists, ids, counts
+
+
+def post_process_l2_static(neighbors, distances, ref_seqs, query_seqs, ref_len, stride, k, query_embeddings,
+                           vectorizer, k_clusters):
+    """post_process_l2_static (src/utils/post_processor.cpp:1023-1162), the reference's live rerank
+    (src/main.cpp:330): flattened (final_seqs, final_dists, final_ids), k_clusters rows per query
+    (batch_reranker is called with k = k_clusters; `k` and `query_seqs` are unused there too). ref_seqs is a
+    WindowTable or a list of windows; vectorizer an Encoder (embeds the table once on the device)."""
+    table = ref_seqs if isinstance(ref_seqs, WindowTable) else WindowTable(ref_seqs)
+    if window_embeddings_ptr(table)[0] == 0:
+        embed_windows(table, getattr(vectorizer, "encoder", vectorizer))
+    nb = np.asarray([list(r) for r in neighbors], dtype=np.int64) if not isinstance(neighbors, np.ndarray) else neighbors
+    try:
+        dists, ids, counts = l2_rerank_arrays(table, nb, query_embeddings, stride, k_clusters)
+    except DrmError as e:
+        raise RuntimeError(str(e)) from e
+    seqs, dd, fid = [], [], []
+    for i in range(len(counts)):
+        for j in range(int(counts[i])):
+            wid = int(ids[i, j])
+            dd.append(float(dists[i, j]))
+            fid.append(wid)
+            if not isinstance(ref_seqs, WindowTable):
+                seqs.append(ref_seqs[wid])
+    return seqs, dd, fid

@@ -32,6 +32,7 @@ extern "C" {
  * counters (drm_*_overflows / _fallbacks) describe the handle's most recent search. */
 typedef struct drm_index drm_index; /* device-resident IndexHNSWPQ */
 typedef struct drm_refs drm_refs;   /* device-resident static window table (ref_seqs) */
+typedef struct drm_encoder drm_encoder; /* device-resident GRU read encoder */
 
 typedef struct {
     int32_t d;             /* vector dimension                                  */
@@ -192,6 +193,34 @@ int drm_post_process_sw_static_device(drm_refs *refs, const int64_t *d_neighbors
                                       int64_t stride, int32_t k, int32_t k_clusters, int32_t *d_top_scores,
                                       uint64_t *d_top_ids, int32_t *d_status, void *stream);
 
+/* ---------------------------------------------------------------- L2 rerank (the reference's live path)
+ * post_process_l2_static (src/utils/post_processor.cpp:1023-1162, called at src/main.cpp:330) ->
+ * find_sequences (static) -> Vectorizer::vectorize of the candidate windows -> batch_reranker(k = k_clusters)
+ * (src/utils/reranker.cpp:98-195) -> calc_l2_dist (src/utils/metrics.cpp:48-61).
+ * drm_refs_embed fills a device table of every window's embedding with the read encoder (the reference
+ * re-embeds each candidate window per run; the encoder is a deterministic function of the window, so the
+ * table row is the same vector) -- n_ref x 128 f32 of HBM, synchronous on `stream`. Encoder and window
+ * table must be on the same device. drm_refs_embeddings returns the table's device pointer (NULL before
+ * drm_refs_embed) and its width. */
+int drm_refs_embed(drm_refs *refs, drm_encoder *enc, void *stream);
+int drm_refs_embeddings(drm_refs *refs, const float **d_emb, int32_t *dim);
+/* neighbors [nq x kk] (every label is a candidate, as in the reference), query_emb [nq x d] f32 (the search's
+ * query embeddings). Outputs [nq x k_clusters]: top_dists (sqrtf of the rounded squares summed in index order, ascending,
+ * libstdc++ std::partial_sort's order among ties), top_ids (window ids), counts[nq] (k_clusters, or 0 for
+ * kk == 0). stride > 1 reproduces the reference's global expansion stream (query q reranks stream entries
+ * [q*kk*stride, (q+1)*kk*stride) of the whole call), so such a call must not be split into batches.
+ * Errors: DRM_ERR_ARG "Invalid mapping index in expansion" (a label outside the table, or a range past the
+ * stream: the reference throws or reads out of bounds), DRM_ERR_CANDS (kk*stride < k_clusters); *bad_query
+ * receives the first offending query. Host pointers. */
+int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const float *query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                               float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query);
+/* Device-buffer form on `stream`; d_status[nq]: k_clusters or 0 = rows emitted, -1 = not enough candidates,
+ * -4 = invalid label / range past the stream. */
+int drm_post_process_l2_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const float *d_query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                                      float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream);
+
 /* ---------------------------------------------------------------- batch executor (exec.cpp)
  * Pinned host memory: buffers from drm_host_alloc make the executor's host <-> device copies DMA
  * transfers that overlap the kernels; ordinary (pageable) buffers work too, staged by the runtime. */
@@ -313,7 +342,6 @@ int drm_embed_kmer3_device(const uint8_t *d_rows, int64_t n, int32_t len, int64_
  * Preprocessor::preprocess tokens (src/inference/preprocess.cpp:20-42) + the OpenVINO GRU model
  * (src/inference/fast_model.cpp:3-68, models/finetuned_sgn33-new-a-Apr6.xml) on the GPU.
  * -------------------------------------------------------------------------------------------*/
-typedef struct drm_encoder drm_encoder;
 typedef struct {
     int32_t hidden, emb_dim, max_len, out_dim; /* 64, 64, 123 (config.hpp:21), 128 (config.hpp:22) */
     int32_t n_token_rows;                     /* 97: padding + the 96 _Tok2Index tokens */

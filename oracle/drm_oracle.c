@@ -813,3 +813,189 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
     }
     return 0;
 }
+
+/* ========================================================================================
+ * L2 rerank: post_process_l2_static (src/utils/post_processor.cpp:1023-1162) -> find_sequences
+ * (static, :204-336) -> batch_reranker (src/utils/reranker.cpp:98-195, k = k_clusters) ->
+ * calc_l2_dist (src/utils/metrics.cpp:48-61). Candidate embeddings are rows of emb[n_ref x d].
+ * ====================================================================================== */
+
+/* calc_l2_dist as g++ -O3 -march=native builds the reference (build.zig:48-57), read off the reference's own
+ * metrics.cpp compiled with -mavx2 -mfma (oracle/_ref): the loop is vectorized as vsubps + vmulps over
+ * 8-float blocks (then one 4-float block) whose squares are added to `sum` one at a time in index order
+ * (vaddss: an in-order reduction, no contraction); only the last <= 3 elements run as scalar
+ * vfmadd231ss. mode 0: every square rounded, then added (the vector body; all of d = 128);
+ * mode 1: every element fused; mode 2: the -mavx2 schedule above (fused scalar tail). */
+float oracle_calc_l2_dist(const float *cand, const float *query, int64_t d, int mode)
+{
+    int64_t n_unfused = d;
+    if (mode == 1)
+        n_unfused = 0;
+    else if (mode == 2) {
+        const int64_t n8 = d >= 8 ? d / 8 * 8 : 0;
+        n_unfused = n8 + (d - n8 >= 4 ? 4 : 0);
+    }
+    float sum = 0.0f;
+    for (int64_t i = 0; i < d; ++i) {
+        const float diff = cand[i] - query[i];
+        if (i >= n_unfused)
+            sum = fmaf(diff, diff, sum);
+        else {
+            const float sq = diff * diff;
+            sum = sum + sq;
+        }
+    }
+    return sqrtf(sum);
+}
+
+/* libstdc++ std::partial_sort with comp(a, b) := dists[a] < dists[b] (reranker.cpp:165-166) */
+#define PSL_COMP(a, b) (dists[(a)] < dists[(b)])
+
+static void psl_adjust_heap(int64_t *first, int64_t hole, int64_t len, int64_t value, const float *dists)
+{
+    const int64_t top = hole;
+    int64_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (PSL_COMP(first[second], first[second - 1]))
+            second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top && PSL_COMP(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+void oracle_partial_sort_asc_f32(int64_t *idx, int64_t n, int64_t k, const float *dists)
+{
+    if (k <= 0)
+        return;
+    if (k >= 2) {
+        int64_t parent = (k - 2) / 2;
+        for (;;) {
+            psl_adjust_heap(idx, parent, k, idx[parent], dists);
+            if (parent == 0)
+                break;
+            parent--;
+        }
+    }
+    for (int64_t i = k; i < n; ++i)
+        if (PSL_COMP(idx[i], idx[0])) {
+            const int64_t v = idx[i];
+            idx[i] = idx[0];
+            psl_adjust_heap(idx, 0, k, v, dists);
+        }
+    for (int64_t last = k - 1; last > 0; --last) {
+        const int64_t v = idx[last];
+        idx[last] = idx[0];
+        psl_adjust_heap(idx, 0, last, v, dists);
+    }
+}
+
+/* find_sequences' sparse expansion of one label (size_t arithmetic, :248-258) */
+static void l2_expand(uint64_t id, uint64_t s, uint64_t n, uint64_t *start, uint64_t *cnt)
+{
+    const uint64_t actual = id * s;
+    if (actual >= n) {
+        *start = 0;
+        *cnt = 0;
+        return;
+    }
+    *start = actual >= s - 1 ? actual - s + 1 : 0;
+    *cnt = (actual + s < n ? actual + s : n) - *start;
+}
+
+/* Returns 0, or -(q+1) for the first query whose candidate range is invalid (a dense label >= n_ref,
+ * or a sparse range past the expanded stream), or -(nq+1+q) for the first query with fewer than
+ * k_clusters candidates. Outputs [nq x k_clusters]; status[q] = k_clusters / 0 / -1 / -4 as the device. */
+int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d, const int64_t *neighbors, int64_t nq,
+                                      int64_t kk, const float *query_emb, int64_t stride, int64_t k_clusters,
+                                      int mode, float *top_dists, uint64_t *top_ids, int32_t *status)
+{
+    const int64_t nc = stride == 1 ? kk : kk * stride;
+    /* the global expansion stream of the whole call (sparse): one entry per expanded window */
+    uint64_t *stream = NULL;
+    uint64_t total = 0;
+    if (stride > 1) {
+        for (int64_t i = 0; i < nq * kk; ++i) {
+            uint64_t st, c;
+            l2_expand((uint64_t)neighbors[i], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
+            total += c;
+        }
+        stream = (uint64_t *)malloc(sizeof(uint64_t) * (total ? total : 1));
+        uint64_t w = 0;
+        for (int64_t i = 0; i < nq * kk; ++i) {
+            uint64_t st, c;
+            l2_expand((uint64_t)neighbors[i], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
+            for (uint64_t t = 0; t < c; ++t)
+                stream[w++] = st + t;
+        }
+    }
+    float *dists = (float *)malloc(sizeof(float) * (nc ? nc : 1));
+    uint64_t *cand = (uint64_t *)malloc(sizeof(uint64_t) * (nc ? nc : 1));
+    int64_t *idx = (int64_t *)malloc(sizeof(int64_t) * (nc ? nc : 1));
+    int64_t first_invalid = -1, first_short = -1;
+    for (int64_t q = 0; q < nq; ++q) {
+        int ok = 1;
+        for (int64_t c = 0; c < nc && ok; ++c) {
+            if (stride == 1) {
+                cand[c] = (uint64_t)neighbors[q * kk + c];
+                ok = cand[c] < (uint64_t)n_ref;
+            } else {
+                const uint64_t g = (uint64_t)q * (uint64_t)nc + (uint64_t)c;
+                ok = g < total;
+                if (ok)
+                    cand[c] = stream[g];
+            }
+        }
+        int32_t st;
+        if (!ok)
+            st = -4;
+        else if (nc == 0)
+            st = 0;
+        else if (nc < k_clusters)
+            st = -1;
+        else
+            st = (int32_t)k_clusters;
+        status[q] = st;
+        if (st == -4 && first_invalid < 0)
+            first_invalid = q;
+        if (st == -1 && first_short < 0)
+            first_short = q;
+        if (st > 0) {
+            for (int64_t c = 0; c < nc; ++c) {
+                dists[c] = oracle_calc_l2_dist(emb + cand[c] * (uint64_t)d, query_emb + q * d, d, mode);
+                idx[c] = c;
+            }
+            oracle_partial_sort_asc_f32(idx, nc, k_clusters, dists);
+            for (int64_t j = 0; j < k_clusters; ++j) {
+                top_dists[q * k_clusters + j] = dists[idx[j]];
+                top_ids[q * k_clusters + j] = cand[idx[j]];
+            }
+        } else {
+            for (int64_t j = 0; j < k_clusters; ++j) {
+                top_dists[q * k_clusters + j] = -1.0f;
+                top_ids[q * k_clusters + j] = ~0ull;
+            }
+        }
+    }
+    free(stream);
+    free(dists);
+    free(cand);
+    free(idx);
+    if (first_invalid >= 0)
+        return -(first_invalid + 1);
+    if (first_short >= 0)
+        return -(nq + 1 + first_short);
+    return 0;
+}

@@ -78,6 +78,13 @@ int oracle_hnswpq_search(const oracle_hnswpq_t *ix, const float *x, int64_t n, i
  * pop_min calls facing an equal valid minimum, queries with at least one such pop_min */
 void oracle_hnsw_counters(int64_t *out6);
 
+/* L2 rerank: post_process_l2_static -> batch_reranker -> calc_l2_dist (see drm_oracle.c) */
+float oracle_calc_l2_dist(const float *cand, const float *query, int64_t d, int mode);
+void oracle_partial_sort_asc_f32(int64_t *idx, int64_t n, int64_t k, const float *dists);
+int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d, const int64_t *neighbors, int64_t nq,
+                                      int64_t kk, const float *query_emb, int64_t stride, int64_t k_clusters,
+                                      int mode, float *top_dists, uint64_t *top_ids, int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,10 @@ def lib():
         _lib.oracle_post_process_sw_dynamic.restype = C.c_int64
         _lib.oracle_hnswpq_search.restype = C.c_int
         _lib.oracle_pq_distance_table.restype = None
+        _lib.oracle_calc_l2_dist.restype = C.c_float
+        _lib.oracle_calc_l2_dist.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int]
+        _lib.oracle_partial_sort_asc_f32.restype = None
+        _lib.oracle_post_process_l2_static.restype = C.c_int64
     return _lib
 
 
@@ -35,6 +39,7 @@ def stl():
     if _stl is None:
         _stl = C.CDLL(os.path.join(_HERE, "libstl_sort.so"))
         _stl.stl_partial_sort_desc.restype = None
+        _stl.stl_partial_sort_asc_f32.restype = None
     return _stl
 
 
@@ -48,6 +53,9 @@ def ref():
         _ref = C.CDLL(os.path.join(_HERE, "_ref", "libdrm_ref.so"))
         _ref.ref_calc_sw_score.restype = C.c_int
         _ref.ref_calc_sw_score.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
+        if hasattr(_ref, "ref_calc_l2_dist"):
+            _ref.ref_calc_l2_dist.restype = C.c_float
+            _ref.ref_calc_l2_dist.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     return _ref
 
 
@@ -218,3 +226,51 @@ def hnswlib_search(fx, q, k, ef, nthreads=0):
         C.c_int(nthreads))
     assert rc == 0
     return D, I, nd, nh
+
+
+# ------------------------------------------------------------------ L2 rerank (post_process_l2_static)
+def calc_l2_dist(cand, query, mode=2):
+    """calc_l2_dist (src/utils/metrics.cpp:48-61) restated (drm_oracle.c): mode 2 = the reference's g++
+    -O3 -march=native schedule (vector body: rounded squares added in order; scalar tail fused), 0 = no
+    fusion (identical to 2 when d % 4 == 0, e.g. the model's d = 128), 1 = every element fused."""
+    a = np.ascontiguousarray(cand, dtype=np.float32)
+    b = np.ascontiguousarray(query, dtype=np.float32)
+    return float(lib().oracle_calc_l2_dist(a.ctypes.data, b.ctypes.data, len(a), int(mode)))
+
+
+def ref_calc_l2_dist(cand, query):
+    """The reference's own calc_l2_dist (oracle/_ref, built with -mavx2 -mfma)."""
+    a = np.ascontiguousarray(cand, dtype=np.float32)
+    b = np.ascontiguousarray(query, dtype=np.float32)
+    return float(ref().ref_calc_l2_dist(a.ctypes.data, b.ctypes.data, len(a)))
+
+
+def partial_sort_asc_f32(dists, k):
+    dists = np.ascontiguousarray(dists, dtype=np.float32)
+    idx = np.arange(len(dists), dtype=np.int64)
+    lib().oracle_partial_sort_asc_f32(_p(idx, C.c_int64), C.c_int64(len(dists)), C.c_int64(k), _p(dists, C.c_float))
+    return idx[:k]
+
+
+def stl_partial_sort_asc_f32(dists, k):
+    dists = np.ascontiguousarray(dists, dtype=np.float32)
+    idx = np.zeros(len(dists), dtype=np.int64)
+    stl().stl_partial_sort_asc_f32(_p(idx, C.c_int64), C.c_int64(len(dists)), C.c_int64(k), _p(dists, C.c_float))
+    return idx[:k]
+
+
+def post_process_l2_static(emb, neighbors, query_emb, stride, k_clusters, mode=2):
+    """post_process_l2_static -> batch_reranker(k = k_clusters) over window embeddings emb [n_ref, d].
+    Returns (rc, dists [nq, k_clusters], ids [nq, k_clusters] u64, status [nq]); rc as the C oracle."""
+    emb = np.ascontiguousarray(emb, dtype=np.float32)
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    qe = np.ascontiguousarray(query_emb, dtype=np.float32)
+    nq, kk = nb.shape
+    dists = np.zeros((nq, k_clusters), dtype=np.float32)
+    ids = np.zeros((nq, k_clusters), dtype=np.uint64)
+    status = np.zeros(nq, dtype=np.int32)
+    rc = lib().oracle_post_process_l2_static(
+        _p(emb, C.c_float), C.c_int64(emb.shape[0]), C.c_int64(emb.shape[1]), _p(nb, C.c_int64), C.c_int64(nq),
+        C.c_int64(kk), _p(qe, C.c_float), C.c_int64(stride), C.c_int64(k_clusters), C.c_int(int(mode)),
+        _p(dists, C.c_float), _p(ids, C.c_uint64), _p(status, C.c_int32))
+    return int(rc), dists, ids, status

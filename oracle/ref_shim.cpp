@@ -13,3 +13,13 @@ extern "C" int ref_calc_sw_score(const uint8_t *s1, int64_t l1, const uint8_t *s
     std::string b(reinterpret_cast<const char *>(s2), (size_t)l2);
     return calc_sw_score(a, b);
 }
+
+// The reference's own calc_l2_dist (src/utils/metrics.cpp:48-61). oracle/Makefile builds this library with
+// -mavx2 -mfma (the features -march=native gives the reference on any current x86 host), so the loop is
+// vectorized and contracted the way the reference's own build compiles it.
+#include <vector>
+extern "C" float ref_calc_l2_dist(const float *a, const float *b, int64_t d)
+{
+    std::vector<float> v1(a, a + d), v2(b, b + d);
+    return calc_l2_dist(v1, v2);
+}
