@@ -273,6 +273,53 @@ def encoder_timing(d_q, Q, q_stride, dev, reps=3):
             "note": "Vectorizer::vectorize on the GPU; not inside `value` (the north star's path starts at embeddings)"}
 
 
+def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
+    """The reference's live post-processing, post_process_l2_static (src/main.cpp:330), on this step's
+    neighbours: drm_refs_embed builds the window-embedding table once (GRU, on the GPU), then
+    drm_post_process_l2_static_device (l2_rerank.hip) is timed with HIP events. Algorithmic bytes per launch:
+    Q*K*(4*128 embedding row + 8 label) + Q*4*128 query + Q*K*(4 + 8) top-k rows (+ the candidate workspace
+    written and re-read, Q*K*12*2). Not inside `value` (the metric's rerank is the SW one)."""
+    from deepreadmapper_amd.encoder import Encoder
+    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream
+    from deepreadmapper_amd.rerank import embed_windows
+    from deepreadmapper_amd._native import check, lib
+    enc = Encoder(device=dev)
+    st = Stream()
+    t0 = time.time()
+    embed_windows(table, enc, st)
+    table_s = time.time() - t0
+    enc.free()
+    d_d, d_i, d_s = DeviceBuffer((Q, K), np.float32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
+
+    def run():
+        check(lib().drm_post_process_l2_static_device(table.handle, d_I.ptr, Q, K, d_x.ptr, 128, 1, K, d_d.ptr,
+                                                      d_i.ptr, d_s.ptr, st.handle))
+    run()
+    st.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = Event(), Event()
+        a.record(st)
+        run()
+        b.record(st)
+        st.synchronize()
+        ts.append(a.elapsed_ms(b))
+    ms = float(np.mean(ts))
+    status = d_s.download()
+    if not (status == K).all():
+        raise SystemExit(f"L2 rerank status != K for {(status != K).sum()} queries")
+    ids = d_i.download()
+    algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + Q * K * 12 * 2
+    gbs = algo / (ms * 1e-3) / 1e9
+    return {"kernel": "l2_dist_kernel + l2_topk_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo},
+            "window_table_embed_s": round(table_s, 2),
+            "truth_top1": round(float(np.mean(ids[:, 0].astype(np.int64) == truth)), 4),
+            "note": "post_process_l2_static on this step's neighbours (the reference's live rerank, whose outputs "
+                    "its main does not save); not inside `value`"}
+
+
 def host_path(ix, table, q_emb, queries, K, EF, flat):
     """The drop-in boundary's own rate (not `value`): drm_search_rerank from pinned host buffers to pinned
     host outputs -- PCIe transfers in, kernels, PCIe transfers out, batches overlapped (exec.cpp) --
@@ -445,6 +492,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the pinned-host drm_search_rerank timing")
     ap.add_argument("--no-encoder", action="store_true", help="skip the GRU read-encoder timing")
+    ap.add_argument("--no-l2", action="store_true", help="skip the L2 rerank (post_process_l2_static) timing")
     ap.add_argument("--embed", choices=["kmer3", "gru"], default=None,
                     help="embeddings of windows and reads: gru (default for c5: the reference's GRU model, run on the "
                          "GPU by drm_vectorize) or kmer3 (the deterministic 3-mer stand-in; default for c3/c4)")
@@ -593,6 +641,7 @@ def main():
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
+    l2 = None if (args.no_l2 or flat) else l2_timing(table, d_I, d_x, Q, K, truth, dev)
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
@@ -639,6 +688,7 @@ def main():
             "host_path": host,
             "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
             if enc else None,
+            "l2_rerank": l2,
             "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),

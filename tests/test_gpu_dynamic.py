@@ -6,6 +6,7 @@
 * the batch executor with a genome handle equals the direct call;
 * bin/pipeline with use_dynamic=1 writes the same .npy files as the static lookup, and with
   use_streaming=1 writes results.sam exactly as write_sam_streaming formats it (src/utils/utils.cpp:409-503)
+  for the rows post_process_l2_dynamic_streaming streams at stride 1 (the first k search neighbours)
   and no .npy files (src/main.cpp:371, :409-412)."""
 import os
 import subprocess
@@ -142,6 +143,9 @@ def test_pipeline_cli_dynamic_and_sam_streaming(tmp_path):
     recs = [(lines[i], lines[i + 1]) for i in range(0, len(lines) - 1, 4) if lines[i].startswith(b"@")]
     qids = [h[1:].split(b" ")[0].split(b"\t")[0].split(b"/")[0].decode() for h, _ in recs]
     reads = [b"<" + s + b">" for _, s in recs]
-    ids = np.load(tmp_path / "static" / "sw_ids.npy")
-    counts = (np.load(tmp_path / "static" / "sw_scores.npy") >= 0).sum(axis=1)
-    assert sam == _sam_ref(qids, reads, ids, counts)
+    # post_process_l2_dynamic_streaming at stride 1 (src/utils/post_processor.cpp:833-878): the first
+    # min(k, k_clusters) = 5 search neighbours in search order, i.e. the static run's indices.npy (save_results
+    # keeps k columns at stride 1)
+    ids = np.load(tmp_path / "static" / "indices.npy")
+    assert ids.shape == (len(reads), 5)
+    assert sam == _sam_ref(qids, reads, ids, np.full(len(reads), 5))

@@ -261,6 +261,18 @@ int main(int argc, char *argv[])
         Pinned<uint64_t> sw_ids(is_npy ? 0 : nq * (size_t)k);
         t0 = clk::now();
         drm_search_stats st{};
+        // The reference streams its SAM from post_process_l2_dynamic_streaming (src/main.cpp:316-319). With a
+        // dense index (stride 1) that function skips every reranker and writes the first min(k, k_clusters)
+        // search neighbours of each query in search order (src/utils/post_processor.cpp:833-878), so the SAM
+        // here comes straight from the search and no rerank runs. A sparse index reranks the expanded windows by
+        // L2 there (:884-1010), which is not built: those SAM rows come from the SW rerank instead.
+        const bool stream_sam = use_streaming && dyn;
+        const bool sam_from_search = stream_sam && stride == 1;
+        if (stream_sam && (size_t)k > (size_t)k_clusters * 2 * stride) // post_processor.cpp:769-772
+            throw drm::Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
+        if (stream_sam && stride > 1)
+            std::cout << "[MAIN] stride > 1: SAM rows from the SW rerank (the reference reranks them by L2 here)"
+                      << std::endl;
         // one pass over queries [lo, lo + m) into the output arrays at row lo
         auto run = [&](size_t lo, size_t m, drm_search_stats *sp) {
             const uint8_t *qb = is_npy ? nullptr : qbuf.p + lo * qs;
@@ -269,12 +281,12 @@ int main(int argc, char *argv[])
                                                ql.p + lo, (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters,
                                                I.p + lo * k_clusters, sw_scores.p + lo * k, sw_ids.p + lo * k,
                                                status.p + lo, sp);
-            return drm_search_rerank(index, rt, x.p + lo * dim, (int64_t)m, (int32_t)dim, k_clusters, ef, qb, ql.p + lo,
+            return drm_search_rerank(index, sam_from_search ? nullptr : rt, x.p + lo * dim, (int64_t)m, (int32_t)dim,
+                                     k_clusters, ef, qb, ql.p + lo,
                                      (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters, I.p + lo * k_clusters,
                                      sw_scores.p + lo * k, sw_ids.p + lo * k, status.p + lo, sp);
         };
         int rc = DRM_OK;
-        const bool stream_sam = use_streaming && dyn;
         if (stream_sam) {
             // post_process_*_dynamic_streaming + write_sam_streaming (src/main.cpp:316-319,
             // src/utils/utils.cpp:409-503): the SAM lines of each block are written by a host thread while the
@@ -300,6 +312,13 @@ int main(int argc, char *argv[])
                     writer = std::thread([&, lo, m] {
                         try {
                             std::vector<int32_t> cnt(m);
+                            if (sam_from_search) {
+                                std::fill(cnt.begin(), cnt.end(), std::min(k, k_clusters));
+                                drm::write_sam_block(sam_file, lo == 0, "ref", ref_len, qseqs, qids, lo, m,
+                                                     reinterpret_cast<const uint64_t *>(I.p) + lo * k_clusters,
+                                                     cnt.data(), (size_t)k_clusters);
+                                return;
+                            }
                             for (size_t i = 0; i < m; ++i)
                                 cnt[i] = std::max(status.p[lo + i], 0);
                             drm::write_sam_block(sam_file, lo == 0, "ref", ref_len, qseqs, qids, lo, m,
