@@ -39,6 +39,7 @@ EXPORTS = [
     "drm_encoder_load", "drm_encoder_export", "drm_encoder_free", "drm_encoder_get_info", "drm_tokenize",
     "drm_vectorize", "drm_vectorize_device", "drm_encoder_flags",
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
+    "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
 ]
 
 
@@ -166,6 +167,9 @@ def lib():
         "drm_refs_embeddings": (C.c_int, [vp, C.POINTER(vp), C.POINTER(i32)]),
         "drm_post_process_l2_static": (C.c_int, [vp, vp, i64, i32, vp, i32, i64, i32, vp, vp, vp, C.POINTER(i64)]),
         "drm_post_process_l2_static_device": (C.c_int, [vp, vp, i64, i32, vp, i32, i64, i32, vp, vp, vp, vp]),
+        "drm_post_process_l2_dynamic": (C.c_int, [vp, vp, i64, i32, vp, i32, i64, i32, i32, vp, vp, vp,
+                                                  C.POINTER(i64)]),
+        "drm_post_process_l2_dynamic_device": (C.c_int, [vp, vp, i64, i32, vp, i32, i64, i32, i32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

@@ -943,10 +943,11 @@ int drm_post_process_sw_dynamic(drm_refs *refs, const int64_t *neighbors, int64_
 }
 
 // ------------------------------------------------------------------------------- L2 rerank
-static drm::L2Args make_l2_args(drm_refs *refs, const int64_t *nb, int64_t nq, int32_t kk, const float *qe, int32_t d,
-                                int64_t stride, int32_t k_clusters, float *td, uint64_t *ti, int32_t *st)
+static drm::L2Args make_l2_args(drm_refs *refs, bool dynamic, const int64_t *nb, int64_t nq, int32_t kk,
+                                const float *qe, int32_t d, int64_t stride, int32_t k, int32_t k_clusters, float *td,
+                                uint64_t *ti, int32_t *st)
 {
-    require_mode(refs, false);
+    require_mode(refs, dynamic);
     if (!refs->dev.emb)
         throw Error(DRM_ERR_ARG, "the window table has no embeddings: call drm_refs_embed first");
     if (d != refs->dev.emb_dim)
@@ -954,83 +955,60 @@ static drm::L2Args make_l2_args(drm_refs *refs, const int64_t *nb, int64_t nq, i
                                      std::to_string(d)); // calc_l2_dist, metrics.cpp:50-53
     if (stride < 1)
         throw Error(DRM_ERR_ARG, "stride must be >= 1");
-    if (nq < 0 || kk < 0 || k_clusters < 0)
-        throw Error(DRM_ERR_ARG, "negative nq / kk / k_clusters");
+    if (nq < 0 || kk < 0 || k_clusters < 0 || k < 0)
+        throw Error(DRM_ERR_ARG, "negative nq / kk / k / k_clusters");
     drm::L2Args a{};
     a.emb = refs->dev.emb;
-    a.n_ref = refs->dev.n_ref;
     a.d = d;
     a.neighbors = nb;
     a.kk = kk;
     a.stride = stride;
     a.query_emb = qe;
-    a.k = k_clusters;
     a.nq = nq;
     a.top_dists = td;
     a.top_ids = ti;
     a.status = st;
+    if (!dynamic) { // post_process_l2_static: every label, kk*stride boundaries, batch_reranker k = k_clusters
+        a.limit = refs->dev.n_ref;
+        a.lpq = kk;
+        a.nc = (int32_t)(stride == 1 ? kk : (int64_t)kk * stride);
+        a.k = k_clusters;
+    } else { // post_process_l2_dynamic(_streaming), stride > 1 (:575-590, :617-627): min(k_clusters, kk) labels,
+             // (2*stride - 1) boundaries per label, positions checked against the genome length, k rows
+        if (stride == 1)
+            throw Error(DRM_ERR_ARG, "post_process_l2_dynamic at stride 1 reranks nothing: its rows are the first "
+                                     "min(k, k_clusters) search neighbours with their search distances");
+        if ((int64_t)k > (int64_t)k_clusters * 2 * stride) // :566-569
+            throw Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
+        a.limit = refs->dev.glen;
+        a.lpq = std::min(k_clusters, kk);
+        a.nc = (int32_t)((int64_t)a.lpq * (2 * stride - 1));
+        a.k = k;
+    }
+    if ((int64_t)a.nc > drm::kMaxCands)
+        throw Error(DRM_ERR_UNSUPPORTED, "more than 1024 candidates per query in the GPU L2 rerank");
     return a;
 }
 
-int drm_refs_embed(drm_refs *refs, drm_encoder *enc, void *stream)
+static int l2_device(bool dynamic, drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                     const float *d_query_emb, int32_t d, int64_t stride, int32_t k, int32_t k_clusters,
+                     float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream)
 {
     return guarded([&] {
-        if (!refs || !enc)
-            throw Error(DRM_ERR_ARG, "null argument");
-        require_mode(refs, false);
-        if (refs->dev.device != enc->dev.device)
-            throw Error(DRM_ERR_ARG, "window table and encoder live on different devices");
-        if (refs->dev.ref_len < 2)
-            throw Error(DRM_ERR_ARG, "windows shorter than 2 bytes cannot be vectorized");
-        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
-        hipStream_t s = (hipStream_t)stream;
-        const int64_t n = refs->dev.n_ref, d = 128;
-        if (!refs->dev.emb)
-            DRM_HIP_CHECK(drm::malloc_big((void **)&refs->dev.emb, sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d,
-                                          drm::kBigWindows));
-        refs->dev.emb_dim = (int32_t)d;
-        const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), (int64_t)4 << 20);
-        DevBuf<int32_t> lens((size_t)chunk);
-        {
-            std::vector<int32_t> h((size_t)chunk, refs->dev.ref_len);
-            lens.upload(h.data());
-        }
-        for (int64_t r0 = 0; r0 < n; r0 += chunk)
-            drm::launch_encode(enc->dev, refs->dev.windows + r0 * refs->dev.row_stride, lens.p,
-                               std::min(chunk, n - r0), refs->dev.row_stride, refs->dev.emb + r0 * d, s);
-        DRM_HIP_CHECK(hipStreamSynchronize(s));
-    });
-}
-
-int drm_refs_embeddings(drm_refs *refs, const float **d_emb, int32_t *dim)
-{
-    return guarded([&] {
-        if (!refs || !d_emb)
-            throw Error(DRM_ERR_ARG, "null argument");
-        *d_emb = refs->dev.emb;
-        if (dim)
-            *dim = refs->dev.emb_dim;
-    });
-}
-
-int drm_post_process_l2_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
-                                      const float *d_query_emb, int32_t d, int64_t stride, int32_t k_clusters,
-                                      float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream)
-{
-    return guarded([&] {
-        drm::L2Args a = make_l2_args(refs, d_neighbors, nq, kk, d_query_emb, d, stride, k_clusters, d_top_dists,
-                                     d_top_ids, d_status);
+        drm::L2Args a = make_l2_args(refs, dynamic, d_neighbors, nq, kk, d_query_emb, d, stride, k, k_clusters,
+                                     d_top_dists, d_top_ids, d_status);
         DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
         drm::launch_l2_rerank(refs->dev, a, (hipStream_t)stream);
     });
 }
 
-int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
-                               const float *query_emb, int32_t d, int64_t stride, int32_t k_clusters,
-                               float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query)
+static int l2_host(bool dynamic, drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                   const float *query_emb, int32_t d, int64_t stride, int32_t k, int32_t k_clusters, float *top_dists,
+                   uint64_t *top_ids, int32_t *counts, int64_t *bad_query)
 {
     return guarded([&] {
-        drm::L2Args a = make_l2_args(refs, nullptr, nq, kk, nullptr, d, stride, k_clusters, nullptr, nullptr, nullptr);
+        drm::L2Args a = make_l2_args(refs, dynamic, nullptr, nq, kk, nullptr, d, stride, k, k_clusters, nullptr,
+                                     nullptr, nullptr);
         if (bad_query)
             *bad_query = -1;
         if (nq <= 0)
@@ -1038,10 +1016,11 @@ int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t
         if (!neighbors || !query_emb || !top_dists || !top_ids || !counts)
             throw Error(DRM_ERR_ARG, "null argument");
         DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        const size_t rows = (size_t)nq * (size_t)a.k;
         DevBuf<int64_t> dn((size_t)nq * kk);
-        DevBuf<float> dqe((size_t)nq * d), dd((size_t)nq * k_clusters);
+        DevBuf<float> dqe((size_t)nq * d), dd(rows);
         DevBuf<int32_t> dst((size_t)nq);
-        DevBuf<uint64_t> di((size_t)nq * k_clusters);
+        DevBuf<uint64_t> di(rows);
         if (dn.n)
             dn.upload(neighbors);
         dqe.upload(query_emb);
@@ -1076,12 +1055,100 @@ int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t
         if (first_bad >= 0) {
             if (bad_query)
                 *bad_query = first_bad;
-            const int64_t nc = stride == 1 ? (int64_t)kk : (int64_t)kk * stride;
-            throw Error(DRM_ERR_CANDS, "Not enough candidates (" + std::to_string(nc) + " < " +
-                                           std::to_string(k_clusters) + ") for query " +
+            throw Error(DRM_ERR_CANDS, "Not enough candidates (" + std::to_string(a.nc) + " < " +
+                                           std::to_string(a.k) + ") for query " +
                                            std::to_string(first_bad)); // reranker.cpp:154-158
         }
     });
+}
+
+int drm_refs_embed(drm_refs *refs, drm_encoder *enc, void *stream)
+{
+    return guarded([&] {
+        if (!refs || !enc)
+            throw Error(DRM_ERR_ARG, "null argument");
+        if (refs->dev.device != enc->dev.device)
+            throw Error(DRM_ERR_ARG, "window table and encoder live on different devices");
+        if (refs->dev.ref_len < 2)
+            throw Error(DRM_ERR_ARG, "windows shorter than 2 bytes cannot be vectorized");
+        DRM_HIP_CHECK(hipSetDevice(refs->dev.device));
+        hipStream_t s = (hipStream_t)stream;
+        const bool genome = refs->dev.genome != nullptr;
+        // a genome handle: windows [0, glen), the positions the dynamic sparse expansion can reach
+        const int64_t n = genome ? refs->dev.glen : refs->dev.n_ref, d = 128;
+        if (refs->dev.emb && refs->dev.emb_rows != n) {
+            DRM_HIP_CHECK(hipFree(refs->dev.emb));
+            refs->dev.emb = nullptr;
+        }
+        if (!refs->dev.emb)
+            DRM_HIP_CHECK(drm::malloc_big((void **)&refs->dev.emb, sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d,
+                                          drm::kBigWindows));
+        refs->dev.emb_dim = (int32_t)d;
+        refs->dev.emb_rows = n;
+        const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), (int64_t)4 << 20);
+        DevBuf<int32_t> lens((size_t)chunk);
+        const int64_t rs = std::max<int64_t>(16, ((int64_t)refs->dev.ref_len + 15) / 16 * 16);
+        DevBuf<uint8_t> rows(genome ? (size_t)chunk * (size_t)rs : 0);
+        if (!genome) {
+            std::vector<int32_t> h((size_t)chunk, refs->dev.ref_len);
+            lens.upload(h.data());
+        }
+        for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+            const int64_t m = std::min(chunk, n - r0);
+            if (genome) {
+                drm::launch_genome_rows(refs->dev, r0, m, rows.p, rs, lens.p, s);
+                drm::launch_encode(enc->dev, rows.p, lens.p, m, rs, refs->dev.emb + r0 * d, s);
+            } else {
+                drm::launch_encode(enc->dev, refs->dev.windows + r0 * refs->dev.row_stride, lens.p, m,
+                                   refs->dev.row_stride, refs->dev.emb + r0 * d, s);
+            }
+        }
+        DRM_HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int drm_refs_embeddings(drm_refs *refs, const float **d_emb, int32_t *dim)
+{
+    return guarded([&] {
+        if (!refs || !d_emb)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *d_emb = refs->dev.emb;
+        if (dim)
+            *dim = refs->dev.emb_dim;
+    });
+}
+
+int drm_post_process_l2_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                      const float *d_query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                                      float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream)
+{
+    return l2_device(false, refs, d_neighbors, nq, kk, d_query_emb, d, stride, k_clusters, k_clusters, d_top_dists,
+                     d_top_ids, d_status, stream);
+}
+
+int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                               const float *query_emb, int32_t d, int64_t stride, int32_t k_clusters,
+                               float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query)
+{
+    return l2_host(false, refs, neighbors, nq, kk, query_emb, d, stride, k_clusters, k_clusters, top_dists, top_ids,
+                   counts, bad_query);
+}
+
+int drm_post_process_l2_dynamic_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                       const float *d_query_emb, int32_t d, int64_t stride, int32_t k,
+                                       int32_t k_clusters, float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status,
+                                       void *stream)
+{
+    return l2_device(true, refs, d_neighbors, nq, kk, d_query_emb, d, stride, k, k_clusters, d_top_dists, d_top_ids,
+                     d_status, stream);
+}
+
+int drm_post_process_l2_dynamic(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                                const float *query_emb, int32_t d, int64_t stride, int32_t k, int32_t k_clusters,
+                                float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query)
+{
+    return l2_host(true, refs, neighbors, nq, kk, query_emb, d, stride, k, k_clusters, top_dists, top_ids, counts,
+                   bad_query);
 }
 
 } // extern "C"

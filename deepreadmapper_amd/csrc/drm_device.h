@@ -223,10 +223,11 @@ struct DeviceRefs {
     // table; window id w is genome[w / 2 ..+ ref_len), reverse-complemented when w is odd
     uint8_t *genome = nullptr;
     int64_t glen = 0;
-    // L2 rerank (post_process_l2_static): the read encoder's embedding of every window,
-    // [n_ref][emb_dim] f32, filled once by drm_refs_embed (l2_rerank.hip)
+    // L2 rerank (post_process_l2_*): the read encoder's embedding of every window, [emb_rows][emb_dim] f32,
+    // filled once by drm_refs_embed (l2_rerank.hip); emb_rows = n_ref, or glen for a genome handle
     float *emb = nullptr;
     int32_t emb_dim = 0;
+    int64_t emb_rows = 0;
 };
 
 struct RerankArgs {
@@ -267,20 +268,26 @@ void launch_sw_pairs(const uint8_t *d_s1, const int64_t *d_off1, const int32_t *
 // L2 rerank (post_process_l2_static -> batch_reranker, src/utils/post_processor.cpp:1023-1162,
 // src/utils/reranker.cpp:98-195): distances from the window embedding table, libstdc++ partial_sort
 struct L2Args {
-    const float *emb;          // [n_ref][d] window embeddings
-    int64_t n_ref;
+    const float *emb;          // [limit][d] window embeddings (row = window id)
+    int64_t limit;             // ids / expanded positions must be < limit: n_ref, or the genome length (dynamic)
     int32_t d;
     const int64_t *neighbors;  // [nq][kk]
     int32_t kk;
+    int32_t lpq;               // labels used per query: kk (static), min(k_clusters, kk) (dynamic sparse)
+    int32_t nc;                // candidates per query: kk at stride 1, else the boundary width of the caller
     int64_t stride;
     const float *query_emb;    // [nq][d]
-    int32_t k;                 // rows kept per query (batch_reranker's k = k_clusters)
+    int32_t k;                 // rows kept per query (batch_reranker's k)
     int64_t nq;
     float *top_dists;          // [nq][k]
     uint64_t *top_ids;         // [nq][k]
     int32_t *status;           // [nq]
 };
 void launch_l2_rerank(DeviceRefs &refs, L2Args a, hipStream_t stream);
+// genome windows w in [0, n) as rows of ref_len bytes (w / 2 .. + ref_len, reverse-complemented when w is odd;
+// lens[w] = 0 past the genome end), the input of the encoder for a genome handle's embedding table
+void launch_genome_rows(const DeviceRefs &refs, int64_t w0, int64_t n, uint8_t *rows, int64_t row_stride,
+                        int32_t *lens, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------- read encoder
 // HBM image of the GRU read encoder (encoder_gru.hip)

@@ -288,3 +288,20 @@ def post_process_l2_static(neighbors, distances, ref_seqs, query_seqs, ref_len, 
             if not isinstance(ref_seqs, WindowTable):
                 seqs.append(ref_seqs[wid])
     return seqs, dd, fid
+
+
+def l2_rerank_dynamic_arrays(genome_table, neighbors, query_embeddings, stride, k, k_clusters):
+    """post_process_l2_dynamic's rerank (stride > 1) on an embedded GenomeTable: (dists [nq,k] f32,
+    ids [nq,k] u64, counts [nq])."""
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    nq, kk = nb.shape
+    qe = np.ascontiguousarray(query_embeddings, dtype=np.float32)
+    if qe.shape[0] != nq:
+        raise ValueError("one query embedding per neighbor row")
+    dists = np.empty((nq, k), dtype=np.float32)
+    ids = np.empty((nq, k), dtype=np.uint64)
+    counts = np.empty(nq, dtype=np.int32)
+    bad = C.c_int64(-1)
+    check(lib().drm_post_process_l2_dynamic(genome_table.handle, ptr(nb), nq, kk, ptr(qe), qe.shape[1], int(stride),
+                                            int(k), int(k_clusters), ptr(dists), ptr(ids), ptr(counts), C.byref(bad)))
+    return dists, ids, counts

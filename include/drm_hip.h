@@ -220,6 +220,21 @@ int drm_post_process_l2_static(drm_refs *refs, const int64_t *neighbors, int64_t
 int drm_post_process_l2_static_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
                                       const float *d_query_emb, int32_t d, int64_t stride, int32_t k_clusters,
                                       float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status, void *stream);
+/* post_process_l2_dynamic / post_process_l2_dynamic_streaming's rerank (src/utils/post_processor.cpp:553-750,
+ * :752-1021) on a genome handle embedded with drm_refs_embed (a genome handle embeds windows [0, glen): the
+ * positions the sparse expansion can reach, window w = genome[w/2 ..+ ref_len), reverse-complemented for odd
+ * w). stride > 1 only -- at stride 1 the reference reranks nothing and returns the first min(k, k_clusters)
+ * search neighbours with their search distances (DRM_ERR_ARG here). Each query contributes its first
+ * min(k_clusters, kk) labels to one global expansion stream (positions checked against the genome length)
+ * and reranks the stream entries [q*nc, (q+1)*nc), nc = min(k_clusters, kk) * (2*stride - 1), keeping k rows
+ * ([nq x k] outputs). Errors as drm_post_process_l2_static, plus DRM_ERR_K (k > k_clusters*2*stride). */
+int drm_post_process_l2_dynamic(drm_refs *refs, const int64_t *neighbors, int64_t nq, int32_t kk,
+                                const float *query_emb, int32_t d, int64_t stride, int32_t k, int32_t k_clusters,
+                                float *top_dists, uint64_t *top_ids, int32_t *counts, int64_t *bad_query);
+int drm_post_process_l2_dynamic_device(drm_refs *refs, const int64_t *d_neighbors, int64_t nq, int32_t kk,
+                                       const float *d_query_emb, int32_t d, int64_t stride, int32_t k,
+                                       int32_t k_clusters, float *d_top_dists, uint64_t *d_top_ids, int32_t *d_status,
+                                       void *stream);
 
 /* ---------------------------------------------------------------- batch executor (exec.cpp)
  * Pinned host memory: buffers from drm_host_alloc make the executor's host <-> device copies DMA

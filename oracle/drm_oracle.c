@@ -915,31 +915,36 @@ static void l2_expand(uint64_t id, uint64_t s, uint64_t n, uint64_t *start, uint
     *cnt = (actual + s < n ? actual + s : n) - *start;
 }
 
-/* Returns 0, or -(q+1) for the first query whose candidate range is invalid (a dense label >= n_ref,
+/* Shared by the static and dynamic L2 post-processing: each query contributes its first lpq labels to one
+ * expansion stream (stride > 1; positions < limit) and reranks the stream entries [q*nc, (q+1)*nc) with
+ * batch_reranker(k); at stride 1 its candidates are its kk labels (each < limit).
+ * Returns 0, or -(q+1) for the first query whose candidate range is invalid (a dense label >= limit,
  * or a sparse range past the expanded stream), or -(nq+1+q) for the first query with fewer than
- * k_clusters candidates. Outputs [nq x k_clusters]; status[q] = k_clusters / 0 / -1 / -4 as the device. */
-int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d, const int64_t *neighbors, int64_t nq,
-                                      int64_t kk, const float *query_emb, int64_t stride, int64_t k_clusters,
-                                      int mode, float *top_dists, uint64_t *top_ids, int32_t *status)
+ * k candidates. Outputs [nq x k]; status[q] = k / 0 / -1 / -4 as the device. */
+static int64_t l2_rerank_common(const float *emb, int64_t limit, int64_t d, const int64_t *neighbors, int64_t nq,
+                                int64_t kk, int64_t lpq, int64_t nc, const float *query_emb, int64_t stride,
+                                int64_t k_clusters, int mode, float *top_dists, uint64_t *top_ids, int32_t *status)
 {
-    const int64_t nc = stride == 1 ? kk : kk * stride;
+    const int64_t n_ref = limit;
     /* the global expansion stream of the whole call (sparse): one entry per expanded window */
     uint64_t *stream = NULL;
     uint64_t total = 0;
     if (stride > 1) {
-        for (int64_t i = 0; i < nq * kk; ++i) {
-            uint64_t st, c;
-            l2_expand((uint64_t)neighbors[i], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
-            total += c;
-        }
+        for (int64_t q = 0; q < nq; ++q)
+            for (int64_t j = 0; j < lpq; ++j) {
+                uint64_t st, c;
+                l2_expand((uint64_t)neighbors[q * kk + j], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
+                total += c;
+            }
         stream = (uint64_t *)malloc(sizeof(uint64_t) * (total ? total : 1));
         uint64_t w = 0;
-        for (int64_t i = 0; i < nq * kk; ++i) {
-            uint64_t st, c;
-            l2_expand((uint64_t)neighbors[i], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
-            for (uint64_t t = 0; t < c; ++t)
-                stream[w++] = st + t;
-        }
+        for (int64_t q = 0; q < nq; ++q)
+            for (int64_t j = 0; j < lpq; ++j) {
+                uint64_t st, c;
+                l2_expand((uint64_t)neighbors[q * kk + j], (uint64_t)stride, (uint64_t)n_ref, &st, &c);
+                for (uint64_t t = 0; t < c; ++t)
+                    stream[w++] = st + t;
+            }
     }
     float *dists = (float *)malloc(sizeof(float) * (nc ? nc : 1));
     uint64_t *cand = (uint64_t *)malloc(sizeof(uint64_t) * (nc ? nc : 1));
@@ -998,4 +1003,27 @@ int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d
     if (first_short >= 0)
         return -(nq + 1 + first_short);
     return 0;
+}
+
+/* post_process_l2_static (src/utils/post_processor.cpp:1023-1162): all kk labels, boundaries kk*stride per
+ * query, batch_reranker(k = k_clusters) */
+int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d, const int64_t *neighbors, int64_t nq,
+                                      int64_t kk, const float *query_emb, int64_t stride, int64_t k_clusters,
+                                      int mode, float *top_dists, uint64_t *top_ids, int32_t *status)
+{
+    return l2_rerank_common(emb, n_ref, d, neighbors, nq, kk, kk, stride == 1 ? kk : kk * stride, query_emb, stride,
+                            k_clusters, mode, top_dists, top_ids, status);
+}
+
+/* post_process_l2_dynamic(_streaming), stride > 1 (:575-590, :617-627, :884-1010): the first min(k_clusters, kk)
+ * labels, boundaries (2*stride - 1) per label, positions checked against the genome length, batch_reranker(k);
+ * emb rows are the dynamic-lookup windows 0 .. glen-1 */
+int64_t oracle_post_process_l2_dynamic(const float *emb, int64_t glen, int64_t d, const int64_t *neighbors,
+                                       int64_t nq, int64_t kk, const float *query_emb, int64_t stride, int64_t k,
+                                       int64_t k_clusters, int mode, float *top_dists, uint64_t *top_ids,
+                                       int32_t *status)
+{
+    const int64_t lpq = k_clusters < kk ? k_clusters : kk;
+    return l2_rerank_common(emb, glen, d, neighbors, nq, kk, lpq, lpq * (2 * stride - 1), query_emb, stride, k,
+                            mode, top_dists, top_ids, status);
 }

@@ -84,6 +84,10 @@ void oracle_partial_sort_asc_f32(int64_t *idx, int64_t n, int64_t k, const float
 int64_t oracle_post_process_l2_static(const float *emb, int64_t n_ref, int64_t d, const int64_t *neighbors, int64_t nq,
                                       int64_t kk, const float *query_emb, int64_t stride, int64_t k_clusters,
                                       int mode, float *top_dists, uint64_t *top_ids, int32_t *status);
+int64_t oracle_post_process_l2_dynamic(const float *emb, int64_t glen, int64_t d, const int64_t *neighbors,
+                                       int64_t nq, int64_t kk, const float *query_emb, int64_t stride, int64_t k,
+                                       int64_t k_clusters, int mode, float *top_dists, uint64_t *top_ids,
+                                       int32_t *status);
 
 #ifdef __cplusplus
 }

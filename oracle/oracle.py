@@ -31,6 +31,7 @@ def lib():
         _lib.oracle_calc_l2_dist.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int]
         _lib.oracle_partial_sort_asc_f32.restype = None
         _lib.oracle_post_process_l2_static.restype = C.c_int64
+        _lib.oracle_post_process_l2_dynamic.restype = C.c_int64
     return _lib
 
 
@@ -273,4 +274,21 @@ def post_process_l2_static(emb, neighbors, query_emb, stride, k_clusters, mode=2
         _p(emb, C.c_float), C.c_int64(emb.shape[0]), C.c_int64(emb.shape[1]), _p(nb, C.c_int64), C.c_int64(nq),
         C.c_int64(kk), _p(qe, C.c_float), C.c_int64(stride), C.c_int64(k_clusters), C.c_int(int(mode)),
         _p(dists, C.c_float), _p(ids, C.c_uint64), _p(status, C.c_int32))
+    return int(rc), dists, ids, status
+
+
+def post_process_l2_dynamic(emb, neighbors, query_emb, stride, k, k_clusters, mode=2):
+    """post_process_l2_dynamic(_streaming)'s stride > 1 rerank over the dynamic-lookup window embeddings
+    emb [glen, d] (row w = window w). Returns (rc, dists [nq, k], ids [nq, k] u64, status [nq])."""
+    emb = np.ascontiguousarray(emb, dtype=np.float32)
+    nb = np.ascontiguousarray(neighbors, dtype=np.int64)
+    qe = np.ascontiguousarray(query_emb, dtype=np.float32)
+    nq, kk = nb.shape
+    dists = np.zeros((nq, k), dtype=np.float32)
+    ids = np.zeros((nq, k), dtype=np.uint64)
+    status = np.zeros(nq, dtype=np.int32)
+    rc = lib().oracle_post_process_l2_dynamic(
+        _p(emb, C.c_float), C.c_int64(emb.shape[0]), C.c_int64(emb.shape[1]), _p(nb, C.c_int64), C.c_int64(nq),
+        C.c_int64(kk), _p(qe, C.c_float), C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters),
+        C.c_int(int(mode)), _p(dists, C.c_float), _p(ids, C.c_uint64), _p(status, C.c_int32))
     return int(rc), dists, ids, status

@@ -5,10 +5,14 @@ calc_l2_dist build and to libstdc++'s std::partial_sort in tests/test_l2_oracle.
 Bars:
 * window embedding table (drm_refs_embed): bit-identical to drm_vectorize of the same windows;
 * distances and ids: bit-exact against the oracle on the same embedding table, ties included (duplicate
-  labels give exactly equal distances, so the partial_sort tie order is exercised), for k_clusters == kk
-  and < kk, dense and sparse (stride > 1: the reference's global expansion stream);
+  labels give exactly equal distances, so the partial_sort tie order is exercised: those queries go to the
+  heap replay, the others through the sorted fast path), for k_clusters == kk and < kk, 1 to 800
+  candidates per query, dense and sparse (stride > 1: the reference's global expansion stream);
 * errors: a label outside the table -> "Invalid mapping index" (DRM_ERR_ARG), kk*stride < k_clusters ->
-  DRM_ERR_CANDS."""
+  DRM_ERR_CANDS;
+* the dynamic form (post_process_l2_dynamic, stride > 1) on a genome handle: window table rows equal to
+  drm_vectorize of find_sequence's windows (reverse complement for odd ids), reranks bit-exact against the
+  oracle's restatement of its stream and boundaries, and its errors."""
 import ctypes as C
 
 import numpy as np
@@ -77,7 +81,7 @@ def test_l2_static_dense_bitexact(enc, table, nq, kk, kc, seed):
     assert (np.diff(d, axis=1) >= 0).all()
 
 
-@pytest.mark.parametrize("stride,kk,kc", [(3, 8, 8), (4, 16, 30), (2, 32, 64)])
+@pytest.mark.parametrize("stride,kk,kc", [(3, 8, 8), (4, 16, 30), (2, 32, 64), (4, 64, 200), (8, 100, 128)])
 def test_l2_static_sparse_stream_bitexact(enc, table, stride, kk, kc):
     from deepreadmapper_amd.rerank import l2_rerank_arrays
     t, win = table
@@ -88,6 +92,25 @@ def test_l2_static_sparse_stream_bitexact(enc, table, stride, kk, kc):
     qe = enc.vectorize([bytes(win[i]) for i in rng.integers(0, t.n_ref, size=nq)])
     d, ids, counts = l2_rerank_arrays(t, nb, qe, stride, kc)
     rc, wd, wi, st = O.post_process_l2_static(emb, nb, qe, stride, kc)
+    assert rc == 0 and (counts == kc).all()
+    assert np.array_equal(d.view(np.uint32), wd.view(np.uint32))
+    assert np.array_equal(ids, wi)
+
+
+@pytest.mark.parametrize("kc", [128, 37, 1])
+def test_l2_static_tie_heavy(enc, table, kc):
+    """Labels drawn from 6 windows (two of them equal): every query is full of exact distance ties, so the
+    rows come from the libstdc++ heap replay; a few queries without ties take the sorted fast path."""
+    from deepreadmapper_amd.rerank import l2_rerank_arrays
+    t, win = table
+    emb = _download_table(t)
+    rng = np.random.default_rng(kc)
+    nq = 200
+    nb = rng.choice(np.array([5, 6, 7, 8, 9, 10]), size=(nq, 128)).astype(np.int64)
+    nb[:20] = rng.integers(0, t.n_ref, size=(20, 128))  # mostly tie-free
+    qe = enc.vectorize([bytes(win[i]) for i in rng.integers(0, t.n_ref, size=nq)])
+    d, ids, counts = l2_rerank_arrays(t, nb, qe, 1, kc)
+    rc, wd, wi, st = O.post_process_l2_static(emb, nb, qe, 1, kc)
     assert rc == 0 and (counts == kc).all()
     assert np.array_equal(d.view(np.uint32), wd.view(np.uint32))
     assert np.array_equal(ids, wi)
@@ -121,3 +144,100 @@ def test_post_process_l2_static_reference_shape(enc, table):
     assert len(seqs) == len(dists) == len(ids) == 160
     assert all(seqs[i] == refs[ids[i]] for i in range(160))
     assert dists[0] == 0.0 and ids[0] == nb[0, 0]  # the query is window nb[0,0] itself
+
+
+@pytest.fixture(scope="module")
+def genome_table(enc):
+    from deepreadmapper_amd.rerank import GenomeTable, embed_windows
+    rng = np.random.default_rng(21)
+    g = bytes(np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.choice(5, size=6000, p=[.24, .24, .24, .24, .04])])
+    t = GenomeTable(g, 150)
+    embed_windows(t, enc)
+    yield t, g
+    t.free()
+
+
+def _window(g, w, L=150):
+    """find_sequence (src/utils/post_processor.cpp:47-64): window w of the dynamic lookup"""
+    comp = {ord("A"): "T", ord("T"): "A", ord("C"): "G", ord("G"): "C", ord("N"): "N"}
+    pos = w // 2
+    s = g[pos:pos + L]
+    return "".join(comp[c] for c in s[::-1]).encode() if w % 2 else s
+
+
+def test_genome_embedding_table(enc, genome_table):
+    t, g = genome_table
+    emb = _genome_emb(t, len(g))
+    sample = [0, 1, 2, 3, 101, 2999, 3000, len(g) - 1]
+    want = enc.vectorize([_window(g, w) for w in sample])
+    assert np.array_equal(emb[sample], want)
+
+
+def _genome_emb(t, n):
+    from deepreadmapper_amd._native import lib
+    from deepreadmapper_amd.rerank import window_embeddings_ptr
+    p, d = window_embeddings_ptr(t)
+    emb = np.empty((n, d), dtype=np.float32)
+    assert lib().drm_memcpy_d2h(emb.ctypes.data_as(C.c_void_p), C.c_void_p(p), emb.nbytes) == 0
+    return emb
+
+
+@pytest.mark.parametrize("stride,kk,k,kc", [(2, 16, 5, 16), (3, 32, 40, 20), (4, 8, 8, 8)])
+def test_l2_dynamic_sparse_bitexact(enc, genome_table, stride, kk, k, kc):
+    """Interior labels (no clipping): each query reranks its own first min(k_clusters, kk) labels' windows."""
+    from deepreadmapper_amd.rerank import l2_rerank_dynamic_arrays
+    t, g = genome_table
+    emb = _genome_emb(t, len(g))
+    rng = np.random.default_rng(stride * 13 + kk)
+    nq = 80
+    nb = rng.integers(1, (len(g) - stride) // stride, size=(nq, kk)).astype(np.int64)
+    qe = enc.vectorize([_window(g, int(w)) for w in rng.integers(0, len(g), size=nq)])
+    dd, ids, counts = l2_rerank_dynamic_arrays(t, nb, qe, stride, k, kc)
+    rc, wd, wi, st = O.post_process_l2_dynamic(emb, nb, qe, stride, k, kc)
+    assert rc == 0 and (counts == k).all()
+    assert np.array_equal(dd.view(np.uint32), wd.view(np.uint32))
+    assert np.array_equal(ids, wi)
+
+
+def test_l2_dynamic_sparse_clipped_stream(enc, genome_table):
+    """Labels at the genome's ends clip their expansion: the reference's boundaries then straddle queries, and
+    the tail queries run past the stream (status -4). Device form, compared query by query."""
+    from deepreadmapper_amd._native import check, lib
+    from deepreadmapper_amd.device import DeviceBuffer, Stream
+    t, g = genome_table
+    emb = _genome_emb(t, len(g))
+    rng = np.random.default_rng(77)
+    nq, kk, stride, k, kc = 40, 12, 3, 10, 12
+    nb = rng.integers(1, (len(g) - stride) // stride, size=(nq, kk)).astype(np.int64)
+    nb[0, 0], nb[3, 5], nb[7, 2] = 0, len(g) // stride + 5, (len(g) - 1) // stride  # clipped / dropped labels
+    qe = enc.vectorize([_window(g, int(w)) for w in rng.integers(0, len(g), size=nq)])
+    d_nb, d_qe = DeviceBuffer.from_host(nb), DeviceBuffer.from_host(qe)
+    d_d, d_i, d_s = DeviceBuffer((nq, k), np.float32), DeviceBuffer((nq, k), np.uint64), DeviceBuffer(nq, np.int32)
+    st = Stream()
+    check(lib().drm_post_process_l2_dynamic_device(t.handle, d_nb.ptr, nq, kk, d_qe.ptr, 128, stride, k, kc,
+                                                   d_d.ptr, d_i.ptr, d_s.ptr, st.handle))
+    st.synchronize()
+    rc, wd, wi, ws = O.post_process_l2_dynamic(emb, nb, qe, stride, k, kc)
+    status = d_s.download()
+    assert rc < 0 and np.array_equal(status, ws) and (ws == -4).any() and (ws == k).sum() > nq // 2
+    ok = ws == k
+    assert np.array_equal(d_d.download()[ok].view(np.uint32), wd[ok].view(np.uint32))
+    assert np.array_equal(d_i.download()[ok], wi[ok])
+
+
+def test_l2_dynamic_errors(enc, genome_table):
+    from deepreadmapper_amd._native import DRM_ERR_ARG, DRM_ERR_K, DrmError
+    from deepreadmapper_amd.rerank import l2_rerank_dynamic_arrays
+    t, g = genome_table
+    qe = np.zeros((1, 128), np.float32)
+    nb = np.zeros((1, 4), np.int64)
+    with pytest.raises(DrmError) as e:
+        l2_rerank_dynamic_arrays(t, nb, qe, 1, 2, 4)  # stride 1: a pass-through of the search
+    assert e.value.code == DRM_ERR_ARG
+    with pytest.raises(DrmError) as e:
+        l2_rerank_dynamic_arrays(t, nb, qe, 2, 17, 4)  # k > k_clusters * 2 * stride
+    assert e.value.code == DRM_ERR_K
+    nb = np.full((2, 4), len(g), np.int64)  # every label past the genome: an empty stream
+    with pytest.raises(DrmError) as e:
+        l2_rerank_dynamic_arrays(t, nb, np.zeros((2, 128), np.float32), 2, 4, 4)
+    assert e.value.code == DRM_ERR_ARG and "Invalid mapping index" in str(e.value)
