@@ -311,7 +311,7 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     ids = d_i.download()
     algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + Q * K * 12 * 2
     gbs = algo / (ms * 1e-3) / 1e9
-    return {"kernel": "l2_dist_kernel + l2_topk_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
+    return {"kernel": "l2_dist_staged_kernel + l2_sort_kernel (+ l2_topk_kernel for ties)", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo},
             "window_table_embed_s": round(table_s, 2),

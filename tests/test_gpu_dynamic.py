@@ -144,8 +144,8 @@ def test_pipeline_cli_dynamic_and_sam_streaming(tmp_path):
     qids = [h[1:].split(b" ")[0].split(b"\t")[0].split(b"/")[0].decode() for h, _ in recs]
     reads = [b"<" + s + b">" for _, s in recs]
     # post_process_l2_dynamic_streaming at stride 1 (src/utils/post_processor.cpp:833-878): the first
-    # min(k, k_clusters) = 5 search neighbours in search order, i.e. the static run's indices.npy (save_results
-    # keeps k columns at stride 1)
+    # min(k, k_clusters) search neighbours in search order (k = 128 and k_clusters = k at stride 1,
+    # src/main.cpp:54-62), i.e. the static run's indices.npy (save_results keeps k columns at stride 1)
     ids = np.load(tmp_path / "static" / "indices.npy")
-    assert ids.shape == (len(reads), 5)
-    assert sam == _sam_ref(qids, reads, ids, np.full(len(reads), 5))
+    assert ids.shape == (len(reads), 128)
+    assert sam == _sam_ref(qids, reads, ids, np.full(len(reads), 128))

@@ -241,3 +241,25 @@ def test_l2_dynamic_errors(enc, genome_table):
     with pytest.raises(DrmError) as e:
         l2_rerank_dynamic_arrays(t, nb, np.zeros((2, 128), np.float32), 2, 4, 4)
     assert e.value.code == DRM_ERR_ARG and "Invalid mapping index" in str(e.value)
+
+
+def test_pipeline_cli_dynamic_sparse_sam_is_l2(tmp_path):
+    """bin/pipeline use_dynamic=1 use_streaming=1 on a stride-2 index with the GRU model: the SAM rows come from
+    post_process_l2_dynamic_streaming's L2 rerank. Sparse labels run to ~2 * genome length / stride while the
+    expansion keeps only label * stride < genome length, so about half of them expand to nothing; the stream is
+    then shorter than the reference's query boundaries and the reference reads past its arrays for the tail
+    queries. The CLI stops with the reference's error message instead."""
+    import os
+    import subprocess
+    from deepreadmapper_amd.encoder import DEFAULT_MODEL
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fna = os.path.join(root, "tests", "golden", "ecoli_150.fna")
+    fq = os.path.join(root, "tests", "golden", "test_data.fastq")
+    env = dict(os.environ, DRM_BUILD_THREADS="1", DRM_ENCODER=DEFAULT_MODEL)
+    r = subprocess.run([os.path.join(root, "bin", "hnswpq_index"), fna, "s2", "150", "2"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # ef 128, k 10, k_clusters 64 (src/main.cpp:54-62): 64 labels x 3 windows of boundary per query
+    r = subprocess.run([os.path.join(root, "bin", "pipeline"), "s2", fq, fna, "128", "10", "64", "out", "1", "1"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True)
+    assert r.returncode == 1 and "Invalid mapping index" in r.stderr, r.stdout + r.stderr

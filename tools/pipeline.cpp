@@ -264,14 +264,18 @@ int main(int argc, char *argv[])
         // The reference streams its SAM from post_process_l2_dynamic_streaming (src/main.cpp:316-319). With a
         // dense index (stride 1) that function skips every reranker and writes the first min(k, k_clusters)
         // search neighbours of each query in search order (src/utils/post_processor.cpp:833-878), so the SAM
-        // here comes straight from the search and no rerank runs. A sparse index reranks the expanded windows by
-        // L2 there (:884-1010), which is not built: those SAM rows come from the SW rerank instead.
+        // here comes straight from the search and no rerank runs. A sparse index reranks the expanded windows of
+        // the whole run by L2 (:884-1010): drm_post_process_l2_dynamic over every query after the search, on a
+        // window-embedding table of the genome built by the GRU model. Without the model (3-mer stand-in) or
+        // across several devices, those SAM rows come from the SW rerank instead.
         const bool stream_sam = use_streaming && dyn;
         const bool sam_from_search = stream_sam && stride == 1;
+        const bool sam_l2 = stream_sam && stride > 1 && rt && !is_npy && !drm::encoder_model_path().empty();
         if (stream_sam && (size_t)k > (size_t)k_clusters * 2 * stride) // post_processor.cpp:769-772
             throw drm::Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
-        if (stream_sam && stride > 1)
-            std::cout << "[MAIN] stride > 1: SAM rows from the SW rerank (the reference reranks them by L2 here)"
+        if (stream_sam && stride > 1 && !sam_l2)
+            std::cout << "[MAIN] stride > 1 without the GRU model on one device: SAM rows from the SW rerank (the "
+                         "reference reranks them by L2 here)"
                       << std::endl;
         // one pass over queries [lo, lo + m) into the output arrays at row lo
         auto run = [&](size_t lo, size_t m, drm_search_stats *sp) {
@@ -281,13 +285,40 @@ int main(int argc, char *argv[])
                                                ql.p + lo, (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters,
                                                I.p + lo * k_clusters, sw_scores.p + lo * k, sw_ids.p + lo * k,
                                                status.p + lo, sp);
-            return drm_search_rerank(index, sam_from_search ? nullptr : rt, x.p + lo * dim, (int64_t)m, (int32_t)dim,
+            return drm_search_rerank(index, (sam_from_search || sam_l2) ? nullptr : rt, x.p + lo * dim, (int64_t)m,
+                                     (int32_t)dim,
                                      k_clusters, ef, qb, ql.p + lo,
                                      (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters, I.p + lo * k_clusters,
                                      sw_scores.p + lo * k, sw_ids.p + lo * k, status.p + lo, sp);
         };
         int rc = DRM_OK;
-        if (stream_sam) {
+        if (sam_l2) {
+            std::cout << "[MAIN] Using STREAMING output to SAM file: " << sam_file << std::endl;
+            std::filesystem::create_directories(out_dir);
+            rc = run(0, nq, &st);
+            if (rc == DRM_OK) {
+                const auto tl = clk::now();
+                drm_encoder *enc = nullptr;
+                check(drm_encoder_load(drm::encoder_model_path().c_str(), device, &enc));
+                const int erc = drm_refs_embed(rt, enc, nullptr);
+                drm_encoder_free(enc);
+                check(erc);
+                std::vector<float> l2d(nq * (size_t)k);
+                std::vector<uint64_t> l2i(nq * (size_t)k);
+                std::vector<int32_t> cnt(nq);
+                int64_t bad = -1;
+                check(drm_post_process_l2_dynamic(rt, I.p, (int64_t)nq, k_clusters, x.p, (int32_t)dim, (int64_t)stride,
+                                                  k, k_clusters, l2d.data(), l2i.data(), cnt.data(), &bad));
+                std::cout << "[MAIN] L2 rerank (dynamic, stride " << stride << ") time: " << ms_since(tl) << " ms"
+                          << std::endl;
+                size_t block = 1u << 20;
+                if (const char *e = std::getenv("DRM_SAM_BLOCK"))
+                    block = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+                for (size_t lo = 0; lo < nq; lo += block) // write_sam_streaming per reranked batch (:1004-1006)
+                    drm::write_sam_block(sam_file, lo == 0, "ref", ref_len, qseqs, qids, lo, std::min(block, nq - lo),
+                                         l2i.data() + lo * k, cnt.data() + lo, (size_t)k);
+            }
+        } else if (stream_sam) {
             // post_process_*_dynamic_streaming + write_sam_streaming (src/main.cpp:316-319,
             // src/utils/utils.cpp:409-503): the SAM lines of each block are written by a host thread while the
             // GPU works on the next block (blocks of DRM_SAM_BLOCK queries; the file does not depend on it)
