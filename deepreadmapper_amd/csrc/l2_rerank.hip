@@ -73,9 +73,8 @@ __global__ __launch_bounds__(256) void l2_expand_count_kernel(L2Args a, uint64_t
 // (-4 for an invalid label / range; qoff, sparse only: exclusive prefix of the per-query expansion totals). The squares are independent of
 // the summation order, so they are formed from coalesced loads -- 32 lanes read 128 contiguous bytes of one
 // row, two rows per instruction -- and parked in LDS as [row][32 dims] (row stride 33 words: conflict-free);
-// then lane l adds row l's 32 squares in index order to its running sum. Four 32-dim chunks cover d = 128, the next chunk's loads in flight during each chunk's sums.
+// then lane l adds row l's 32 squares in index order to its running sum. Four 32-dim chunks cover d = 128.
 constexpr int kStageRows = 64, kStageDims = 32, kStagePitch = kStageDims + 1;
-constexpr int kEmbDim = 128; // the encoder's output width (config.hpp:22), the only table width
 
 __device__ __forceinline__ bool l2_candidate(const L2Args &a, int64_t q, int c, int nc, const uint64_t *qoff,
                                              uint64_t &pos)
@@ -111,7 +110,7 @@ __device__ __forceinline__ bool l2_candidate(const L2Args &a, int64_t q, int c, 
     return true;
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void l2_dist_staged_kernel(L2Args a, int cmax, int chunks, const uint64_t *qoff,
+__global__ __launch_bounds__(64) void l2_dist_staged_kernel(L2Args a, int cmax, int chunks, const uint64_t *qoff,
                                                             float *cand_dist, uint64_t *cand_ids, int32_t *ncand)
 {
     __shared__ float sq[kStageRows * kStagePitch];
@@ -128,36 +127,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void l2
     row_lo[lane] = (uint32_t)rpos;
     row_hi[lane] = (uint32_t)(rpos >> 32);
     __syncthreads();
-    const float *qv = a.query_emb + q * (int64_t)kEmbDim;
+    const int half = lane >> 5, col = lane & 31;
+    const float *qv = a.query_emb + q * (int64_t)a.d;
     float sum = 0.0f;
-    // one 16-B load per lane covers 8 rows x 128 B: row 8*i + lane/8, dims k0 + 4*(lane%8) .. +3; chunk ch + 1's
-    // row segments are in flight while chunk ch is squared, staged and summed
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const int sub = lane >> 3, quad = (lane & 7) * 4;
-    v4f x[2][kStageRows / 8];
-    auto load_chunk = [&](v4f(&dst)[kStageRows / 8], int k0) {
+    for (int k0 = 0; k0 < a.d; k0 += kStageDims) {
+        const float qx = qv[k0 + col];
+        float x[kStageRows / 2];
 #pragma unroll
-        for (int i = 0; i < kStageRows / 8; ++i) {
-            const int r = 8 * i + sub;
+        for (int rr = 0; rr < kStageRows / 2; ++rr) {
+            const int r = 2 * rr + half;
             const uint64_t p = ((uint64_t)row_hi[r] << 32) | row_lo[r];
-            dst[i] = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(a.emb + p * (uint64_t)kEmbDim + k0 + quad));
+            x[rr] = __builtin_nontemporal_load(a.emb + p * (uint64_t)a.d + k0 + col);
         }
-    };
-    load_chunk(x[0], 0);
 #pragma unroll
-    for (int ch = 0; ch < kEmbDim / kStageDims; ++ch) {
-        const int k0 = ch * kStageDims;
-        if (ch + 1 < kEmbDim / kStageDims)
-            load_chunk(x[(ch + 1) & 1], k0 + kStageDims);
-        const v4f qx = *reinterpret_cast<const v4f *>(qv + k0 + quad);
-#pragma unroll
-        for (int i = 0; i < kStageRows / 8; ++i) {
-            const v4f t = x[ch & 1][i] - qx; // vec1 = candidate, vec2 = query (batch_reranker :150)
-            float *row = sq + (8 * i + sub) * kStagePitch + quad;
-            row[0] = t.x * t.x;
-            row[1] = t.y * t.y;
-            row[2] = t.z * t.z;
-            row[3] = t.w * t.w;
+        for (int rr = 0; rr < kStageRows / 2; ++rr) {
+            const float t = x[rr] - qx; // vec1 = candidate, vec2 = query (batch_reranker :150)
+            sq[(2 * rr + half) * kStagePitch + col] = t * t;
         }
         __syncthreads();
 #pragma unroll
@@ -414,8 +399,8 @@ void launch_l2_rerank(DeviceRefs &refs, L2Args a, hipStream_t stream)
 {
     if (a.nq <= 0)
         return;
-    if (a.d != kEmbDim)
-        throw Error(DRM_ERR_ARG, "the L2 rerank takes 128-d embeddings (the encoder's width)");
+    if (a.d <= 0 || a.d % kStageDims != 0)
+        throw Error(DRM_ERR_ARG, "embedding dimension must be a positive multiple of 32");
     const int64_t nc = a.nc;
     if (nc > kMaxCands)
         throw Error(DRM_ERR_UNSUPPORTED, "more than 1024 candidates per query in the GPU L2 rerank");
