@@ -277,8 +277,9 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     """The reference's live post-processing, post_process_l2_static (src/main.cpp:330), on this step's
     neighbours: drm_refs_embed builds the window-embedding table once (GRU, on the GPU), then
     drm_post_process_l2_static_device (l2_rerank.hip) is timed with HIP events. Algorithmic bytes per launch:
-    Q*K*(4*128 embedding row + 8 label) + Q*4*128 query + Q*K*(4 + 8) top-k rows (+ the candidate workspace
-    written and re-read, Q*K*12*2). Not inside `value` (the metric's rerank is the SW one)."""
+    Q*K*(4*128 embedding row + 8 label) + Q*4*128 query + Q*K*(4 + 8) top-k rows (K <= 128 runs the fused
+    distance + sort kernel, which keeps the candidates on chip). Not inside `value` (the metric's rerank is the
+    SW one)."""
     from deepreadmapper_amd.encoder import Encoder
     from deepreadmapper_amd.device import DeviceBuffer, Event, Stream
     from deepreadmapper_amd.rerank import embed_windows
@@ -309,9 +310,9 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     if not (status == K).all():
         raise SystemExit(f"L2 rerank status != K for {(status != K).sum()} queries")
     ids = d_i.download()
-    algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + Q * K * 12 * 2
+    algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + (Q * K * 12 * 2 if K > 128 else 0)
     gbs = algo / (ms * 1e-3) / 1e9
-    return {"kernel": "l2_dist_staged_kernel + l2_sort_kernel (+ l2_topk_kernel for ties)", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
+    return {"kernel": "l2_fused_kernel (+ l2_topk_kernel for ties)" if K <= 128 else "l2_dist_staged_kernel + l2_sort_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo},
             "window_table_embed_s": round(table_s, 2),

@@ -245,38 +245,9 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <int E>
-__global__ __launch_bounds__(64) void l2_sort_kernel(L2Args a, int cmax, const float *cand_dist,
-                                                     const uint64_t *cand_ids, int32_t *ncand, uint32_t *replay)
+// ascending bitonic sort of 64*E keys held E per lane (slot i = lane + 64 * h)
+template <int E> __device__ __forceinline__ void bitonic_sort(uint64_t (&e)[E], int lane)
 {
-    const int64_t q = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int nc = a.nc;
-    const int st0 = ncand[q];
-    int status;
-    if (st0 == kBadId)
-        status = kBadId;
-    else if (nc == 0)
-        status = 0;
-    else if (nc < a.k)
-        status = -1;
-    else
-        status = a.k;
-    if (status <= 0) {
-        if (lane == 0)
-            a.status[q] = status;
-        for (int j = lane; j < a.k; j += 64) {
-            a.top_dists[q * a.k + j] = -1.0f;
-            a.top_ids[q * a.k + j] = ~0ull;
-        }
-        return;
-    }
-    uint64_t e[E]; // slot i = lane + 64 * h
-#pragma unroll
-    for (int h = 0; h < E; ++h) {
-        const int i = lane + 64 * h;
-        e[h] = i < nc ? ((uint64_t)__float_as_uint(cand_dist[q * cmax + i]) << 32) | (uint32_t)i : ~0ull;
-    }
     constexpr int N = 64 * E;
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1) {
@@ -309,6 +280,11 @@ __global__ __launch_bounds__(64) void l2_sort_kernel(L2Args a, int cmax, const f
             }
         }
     }
+}
+
+// an exact distance tie among sorted positions [0, k] (next(i) = i + 1), for the whole wave
+template <int E> __device__ __forceinline__ bool sorted_tie(const uint64_t (&e)[E], int lane, int k, int nc)
+{
     // exact distance ties among sorted positions [0, k]: next(i) = i + 1
     bool tie = false;
 #pragma unroll
@@ -317,10 +293,47 @@ __global__ __launch_bounds__(64) void l2_sort_kernel(L2Args a, int cmax, const f
         const uint64_t nx_wrap = h + 1 < E ? shfl_u64(e[h + 1 < E ? h + 1 : h], 0) : ~0ull;
         const uint64_t nx = lane < 63 ? nx_same : nx_wrap;
         const int i = lane + 64 * h;
-        if (i < a.k && i + 1 < nc && (uint32_t)(nx >> 32) == (uint32_t)(e[h] >> 32))
+        if (i < k && i + 1 < nc && (uint32_t)(nx >> 32) == (uint32_t)(e[h] >> 32))
             tie = true;
     }
-    if (__any(tie)) {
+    return __any(tie);
+}
+
+template <int E>
+__global__ __launch_bounds__(64) void l2_sort_kernel(L2Args a, int cmax, const float *cand_dist,
+                                                     const uint64_t *cand_ids, int32_t *ncand, uint32_t *replay)
+{
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int nc = a.nc;
+    const int st0 = ncand[q];
+    int status;
+    if (st0 == kBadId)
+        status = kBadId;
+    else if (nc == 0)
+        status = 0;
+    else if (nc < a.k)
+        status = -1;
+    else
+        status = a.k;
+    if (status <= 0) {
+        if (lane == 0)
+            a.status[q] = status;
+        for (int j = lane; j < a.k; j += 64) {
+            a.top_dists[q * a.k + j] = -1.0f;
+            a.top_ids[q * a.k + j] = ~0ull;
+        }
+        return;
+    }
+    uint64_t e[E]; // slot i = lane + 64 * h
+#pragma unroll
+    for (int h = 0; h < E; ++h) {
+        const int i = lane + 64 * h;
+        e[h] = i < nc ? ((uint64_t)__float_as_uint(cand_dist[q * cmax + i]) << 32) | (uint32_t)i : ~0ull;
+    }
+    bitonic_sort<E>(e, lane);
+    const bool tie = sorted_tie<E>(e, lane, a.k, nc);
+    if (tie) {
         if (lane == 0) // replay[0] = count, replay[1 + j] = the j-th handed-over query
             replay[1 + atomicAdd(replay, 1u)] = (uint32_t)q;
         return;
@@ -333,6 +346,102 @@ __global__ __launch_bounds__(64) void l2_sort_kernel(L2Args a, int cmax, const f
         if (i < a.k) {
             a.top_dists[q * a.k + i] = __uint_as_float((uint32_t)(e[h] >> 32));
             a.top_ids[q * a.k + i] = cand_ids[q * cmax + (uint32_t)e[h]];
+        }
+    }
+}
+
+// Kernels 1 + 2 fused for queries of at most 128 candidates (the pipeline's K = 128): a 128-lane block stages
+// and sums the distances of its query (one wave per 64 candidates, as l2_dist_staged_kernel), the keys meet in
+// LDS, and the first wave sorts them (as l2_sort_kernel). The workspace is written only for a query with a tie,
+// for the replay.
+__global__ __launch_bounds__(128) void l2_fused_kernel(L2Args a, int cmax, const uint64_t *qoff, float *cand_dist,
+                                                       uint64_t *cand_ids, uint32_t *replay)
+{
+    __shared__ float sq[2][kStageRows * kStagePitch];
+    __shared__ uint32_t row_lo[128], row_hi[128];
+    __shared__ uint64_t keys[128], cpos[128];
+    __shared__ int bad;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int64_t q = blockIdx.x;
+    const int nc = a.nc;
+    if (tid == 0)
+        bad = 0;
+    __syncthreads();
+    uint64_t pos;
+    const bool ok = l2_candidate(a, q, tid, nc, qoff, pos);
+    if (tid < nc && !ok)
+        bad = 1;
+    const uint64_t rpos = ok ? pos : 0;
+    row_lo[tid] = (uint32_t)rpos;
+    row_hi[tid] = (uint32_t)(rpos >> 32);
+    cpos[tid] = pos;
+    __syncthreads();
+    const int half = lane >> 5, col = lane & 31;
+    const float *qv = a.query_emb + q * (int64_t)a.d;
+    float *sw = sq[w];
+    float sum = 0.0f;
+    for (int k0 = 0; k0 < a.d; k0 += kStageDims) {
+        const float qx = qv[k0 + col];
+        float x[kStageRows / 2];
+#pragma unroll
+        for (int rr = 0; rr < kStageRows / 2; ++rr) {
+            const int r = w * kStageRows + 2 * rr + half;
+            const uint64_t p = ((uint64_t)row_hi[r] << 32) | row_lo[r];
+            x[rr] = __builtin_nontemporal_load(a.emb + p * (uint64_t)a.d + k0 + col);
+        }
+#pragma unroll
+        for (int rr = 0; rr < kStageRows / 2; ++rr) {
+            const float t = x[rr] - qx; // vec1 = candidate, vec2 = query (batch_reranker :150)
+            sw[(2 * rr + half) * kStagePitch + col] = t * t;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kStageDims; ++j)
+            sum = sum + sw[lane * kStagePitch + j];
+        __syncthreads();
+    }
+    const float dist = __builtin_sqrtf(sum);
+    keys[tid] = ok ? ((uint64_t)__float_as_uint(dist) << 32) | (uint32_t)tid : ~0ull;
+    __syncthreads();
+    if (w != 0)
+        return; // no block barrier below this point
+    int status;
+    if (bad)
+        status = kBadId;
+    else if (nc == 0)
+        status = 0;
+    else if (nc < a.k)
+        status = -1;
+    else
+        status = a.k;
+    if (status <= 0) {
+        if (lane == 0)
+            a.status[q] = status;
+        for (int j = lane; j < a.k; j += 64) {
+            a.top_dists[q * a.k + j] = -1.0f;
+            a.top_ids[q * a.k + j] = ~0ull;
+        }
+        return;
+    }
+    uint64_t e[2] = {keys[lane], keys[lane + 64]};
+    bitonic_sort<2>(e, lane);
+    if (sorted_tie<2>(e, lane, a.k, nc)) {
+        for (int c = lane; c < nc; c += 64) { // the replay reads the query's distances and ids
+            cand_dist[q * cmax + c] = __uint_as_float((uint32_t)(keys[c] >> 32));
+            cand_ids[q * cmax + c] = cpos[c];
+        }
+        if (lane == 0)
+            replay[1 + atomicAdd(replay, 1u)] = (uint32_t)q;
+        return;
+    }
+    if (lane == 0)
+        a.status[q] = status;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = lane + 64 * h;
+        if (i < a.k) {
+            a.top_dists[q * a.k + i] = __uint_as_float((uint32_t)(e[h] >> 32));
+            a.top_ids[q * a.k + i] = cpos[(uint32_t)e[h]];
         }
     }
 }
@@ -423,8 +532,9 @@ void launch_l2_rerank(DeviceRefs &refs, L2Args a, hipStream_t stream)
         refs.ws_nq = (size_t)a.nq;
     }
     float *cand_dist = reinterpret_cast<float *>(refs.ws_scores);
-    hipLaunchKernelGGL(l2_fill_status_kernel, dim3((unsigned)((a.nq + 255) / 256)), dim3(256), 0, stream,
-                       refs.ws_ncand, a.nq);
+    if (nc > 128) // the staged distance kernel reports invalid labels through ncand
+        hipLaunchKernelGGL(l2_fill_status_kernel, dim3((unsigned)((a.nq + 255) / 256)), dim3(256), 0, stream,
+                           refs.ws_ncand, a.nq);
     uint64_t *qoff = nullptr;
     void *scan_tmp = nullptr;
     if (a.stride > 1) {
@@ -438,41 +548,37 @@ void launch_l2_rerank(DeviceRefs &refs, L2Args a, hipStream_t stream)
         DRM_HIP_CHECK(hipMallocAsync(&scan_tmp, std::max<size_t>(tmp_bytes, 16), stream));
         DRM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tmp_bytes, qoff, qoff, (int)(a.nq + 1), stream));
     }
-    const int chunks = (int)((nc + kStageRows - 1) / kStageRows);
-    if (nc > 0)
-        hipLaunchKernelGGL(l2_dist_staged_kernel, dim3((unsigned)(a.nq * chunks)), dim3(kStageRows), 0, stream, a,
-                           (int)cmax, chunks, qoff, cand_dist, refs.ws_ids, refs.ws_ncand);
-    DRM_HIP_CHECK(hipGetLastError());
     uint32_t *replay = nullptr; // [0] = count, then the handed-over queries
     DRM_HIP_CHECK(hipMallocAsync((void **)&replay, sizeof(uint32_t) * (size_t)(a.nq + 1), stream));
     DRM_HIP_CHECK(hipMemsetAsync(replay, 0, sizeof(uint32_t), stream));
-    switch (cmax <= 64 ? 1 : cmax <= 128 ? 2 : cmax <= 256 ? 4 : cmax <= 512 ? 8 : 16) {
-    case 1:
-        hipLaunchKernelGGL(l2_sort_kernel<1>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
-                           refs.ws_ids, refs.ws_ncand, replay);
-        break;
-    case 2:
-        hipLaunchKernelGGL(l2_sort_kernel<2>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
-                           refs.ws_ids, refs.ws_ncand, replay);
-        break;
-    case 4:
-        hipLaunchKernelGGL(l2_sort_kernel<4>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
-                           refs.ws_ids, refs.ws_ncand, replay);
-        break;
-    case 8:
-        hipLaunchKernelGGL(l2_sort_kernel<8>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
-                           refs.ws_ids, refs.ws_ncand, replay);
-        break;
-    default:
-        hipLaunchKernelGGL(l2_sort_kernel<16>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
-                           refs.ws_ids, refs.ws_ncand, replay);
-        break;
+    if (nc <= 128) {
+        hipLaunchKernelGGL(l2_fused_kernel, dim3((unsigned)a.nq), dim3(128), 0, stream, a, (int)cmax, qoff, cand_dist,
+                           refs.ws_ids, replay);
+    } else {
+        const int chunks = (int)((nc + kStageRows - 1) / kStageRows);
+        hipLaunchKernelGGL(l2_dist_staged_kernel, dim3((unsigned)(a.nq * chunks)), dim3(kStageRows), 0, stream, a,
+                           (int)cmax, chunks, qoff, cand_dist, refs.ws_ids, refs.ws_ncand);
+        DRM_HIP_CHECK(hipGetLastError());
+        switch (cmax <= 256 ? 4 : cmax <= 512 ? 8 : 16) {
+        case 4:
+            hipLaunchKernelGGL(l2_sort_kernel<4>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
+                               refs.ws_ids, refs.ws_ncand, replay);
+            break;
+        case 8:
+            hipLaunchKernelGGL(l2_sort_kernel<8>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax, cand_dist,
+                               refs.ws_ids, refs.ws_ncand, replay);
+            break;
+        default:
+            hipLaunchKernelGGL(l2_sort_kernel<16>, dim3((unsigned)a.nq), dim3(64), 0, stream, a, (int)cmax,
+                               cand_dist, refs.ws_ids, refs.ws_ncand, replay);
+            break;
+        }
     }
     DRM_HIP_CHECK(hipGetLastError());
     int tpb = 64;
     while (tpb > 1 && (size_t)tpb * (size_t)(cmax + 1) * 8 > 65536)
         tpb >>= 1;
-    const int64_t blocks = std::min<int64_t>((a.nq + tpb - 1) / tpb, 512);
+    const int64_t blocks = std::min<int64_t>((a.nq + tpb - 1) / tpb, 128); // ties are rare: a small grid drains the list
     hipLaunchKernelGGL(l2_topk_kernel, dim3((unsigned)blocks), dim3(tpb), (size_t)tpb * (size_t)(cmax + 1) * 8,
                        stream, a, (int)cmax, cand_dist, refs.ws_ids, replay);
     DRM_HIP_CHECK(hipGetLastError());

@@ -47,7 +47,7 @@ for _ in range(5):
     ts.append(a.elapsed_ms(b))
 assert (d_s.download() == K).all()
 ms = float(np.mean(ts))
-algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + Q * K * 12 * 2
+algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12  # fused path (K <= 128): no workspace
 print(json.dumps({"n_ref": n_ref, "Q": Q, "K": K, "ms": round(ms, 3), "all_ms": [round(x, 3) for x in ts],
                   "embed_s": round(embed_s, 2), "GBps": round(algo / ms / 1e6, 1),
                   "frac": round(algo / ms / 1e6 / 8000, 4)}), flush=True)
