@@ -305,3 +305,46 @@ def l2_rerank_dynamic_arrays(genome_table, neighbors, query_embeddings, stride, 
     check(lib().drm_post_process_l2_dynamic(genome_table.handle, ptr(nb), nq, kk, ptr(qe), qe.shape[1], int(stride),
                                             int(k), int(k_clusters), ptr(dists), ptr(ids), ptr(counts), C.byref(bad)))
     return dists, ids, counts
+
+
+def post_process_l2_dynamic(neighbors, distances, ref_genome, query_seqs, ref_len, stride, k, query_embeddings,
+                            vectorizer, k_clusters):
+    """post_process_l2_dynamic (src/utils/post_processor.cpp:553-750): flattened (final_seqs, final_dists,
+    final_ids). At stride 1 the reference reranks nothing: each query's first min(k, kk) search neighbours with
+    their search distances (:633-660). At stride > 1 the L2 rerank of l2_rerank_dynamic_arrays, k rows per query.
+    ref_genome is the genome string (bytes / str) or a GenomeTable; vectorizer an Encoder or Vectorizer."""
+    g = ref_genome.encode() if isinstance(ref_genome, str) else ref_genome
+    table = g if isinstance(g, GenomeTable) else GenomeTable(g, ref_len)
+    nb = np.asarray([list(r) for r in neighbors], dtype=np.int64) if not isinstance(neighbors, np.ndarray) else neighbors
+
+    def window(wid):
+        if isinstance(g, GenomeTable):
+            return None
+        pos = wid // 2
+        w = g[pos:pos + ref_len] if pos + ref_len <= len(g) else b""
+        if wid % 2 == 1 and w:
+            w = bytes(_COMP_TABLE[np.frombuffer(w, dtype=np.uint8)[::-1]])
+        return bytes(w)
+
+    seqs, dd, fid = [], [], []
+    if stride == 1:
+        for i in range(nb.shape[0]):
+            for j in range(min(k, nb.shape[1])):
+                wid = int(nb[i, j]) & (2**64 - 1)
+                fid.append(wid)
+                dd.append(float(distances[i][j]))
+                seqs.append(window(wid))
+        return seqs, dd, fid
+    if window_embeddings_ptr(table)[0] == 0:
+        embed_windows(table, getattr(vectorizer, "encoder", vectorizer))
+    try:
+        dists, ids, counts = l2_rerank_dynamic_arrays(table, nb, query_embeddings, stride, k, k_clusters)
+    except DrmError as e:
+        raise RuntimeError(str(e)) from e
+    for i in range(len(counts)):
+        for j in range(int(counts[i])):
+            wid = int(ids[i, j])
+            dd.append(float(dists[i, j]))
+            fid.append(wid)
+            seqs.append(window(wid))
+    return seqs, dd, fid

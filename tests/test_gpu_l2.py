@@ -263,3 +263,20 @@ def test_pipeline_cli_dynamic_sparse_sam_is_l2(tmp_path):
     r = subprocess.run([os.path.join(root, "bin", "pipeline"), "s2", fq, fna, "128", "10", "64", "out", "1", "1"],
                        cwd=tmp_path, env=env, capture_output=True, text=True)
     assert r.returncode == 1 and "Invalid mapping index" in r.stderr, r.stdout + r.stderr
+
+
+def test_post_process_l2_dynamic_reference_shape(enc, genome_table):
+    """The reference-shaped dynamic entry: stride 1 passes the first min(k, kk) search neighbours through with
+    their search distances; stride 2 returns the L2 rerank's k rows per query with their windows."""
+    from deepreadmapper_amd import post_process_l2_dynamic
+    t, g = genome_table
+    rng = np.random.default_rng(5)
+    nb = rng.integers(1, (len(g) - 2) // 2, size=(6, 10)).astype(np.int64)
+    dist = rng.random((6, 10)).astype(np.float32)
+    qe = enc.vectorize([_window(g, int(w)) for w in nb[:, 0]])
+    seqs, dd, ids = post_process_l2_dynamic(nb, dist, g, None, 150, 1, 4, qe, enc, 10)
+    assert ids == [int(x) for x in nb[:, :4].reshape(-1)] and dd == [float(x) for x in dist[:, :4].reshape(-1)]
+    assert seqs[0] == _window(g, int(nb[0, 0]))
+    seqs, dd, ids = post_process_l2_dynamic(nb, dist, t, None, 150, 2, 7, qe, enc, 10)
+    assert len(ids) == 42 and all(s is None for s in seqs)
+    assert all(dd[i] <= dd[i + 1] for q in range(6) for i in range(q * 7, q * 7 + 6))
