@@ -52,3 +52,33 @@ def test_c5_search_and_rerank_vs_oracle(c5):
     assert float(np.mean(ids[:, 0].astype(np.int64) == c5["truth"])) > 0.6
     table.free()
     ix.free()
+
+
+def test_c5_l2_rerank_vs_oracle(c5):
+    """post_process_l2_static at full size: the 50M-window GRU embedding table built on the device, the sample's
+    search neighbours reranked by L2 and compared bit-exactly with the oracle on the gathered table rows."""
+    import ctypes as C
+    from deepreadmapper_amd import read_index, WindowTable, Encoder
+    from deepreadmapper_amd._native import lib
+    from deepreadmapper_amd.rerank import embed_windows, l2_rerank_arrays, window_embeddings_ptr
+    from oracle import oracle as O
+    K = EF = 128
+    ix = read_index(c5["index"])
+    _, I, _ = ix.search(c5["x"], K, EF)
+    ix.free()
+    table = WindowTable(c5["refs"])
+    enc = Encoder()
+    embed_windows(table, enc)
+    enc.free()
+    d, ids, cnt = l2_rerank_arrays(table, I, c5["x"], 1, K)
+    # gather the candidates' rows from the device table, relabel the neighbours compactly for the oracle
+    p, dim = window_embeddings_ptr(table)
+    uniq, inv = np.unique(I, return_inverse=True)
+    rows = np.empty((len(uniq), dim), np.float32)
+    for r, w in enumerate(uniq):
+        assert lib().drm_memcpy_d2h(rows[r].ctypes.data_as(C.c_void_p), C.c_void_p(p + int(w) * dim * 4), dim * 4) == 0
+    rc, wd, wi, st = O.post_process_l2_static(rows, inv.reshape(I.shape).astype(np.int64), c5["x"], 1, K)
+    assert rc == 0 and (cnt == K).all()
+    assert np.array_equal(d.view(np.uint32), wd.view(np.uint32))
+    assert np.array_equal(ids, uniq[wi.astype(np.int64)].astype(np.uint64))
+    table.free()
