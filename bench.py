@@ -312,9 +312,15 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     ids = d_i.download()
     algo = float(Q) * K * (4 * 128 + 8) + Q * 4 * 128 + Q * K * 12 + (Q * K * 12 * 2 if K > 128 else 0)
     gbs = algo / (ms * 1e-3) / 1e9
+    # HBM bytes per dispatch from the committed PMC of tools/scripts/l2_bench.py (same Q and K, random labels)
+    prof_path, pmc = committed_pmc("l2_fused_kernel" if K <= 128 else "l2_dist_staged_kernel", "l2_c5shape")
+    traffic = float(pmc["hbm_bytes_est"]) if pmc and "hbm_bytes_est" in pmc else None
     return {"kernel": "l2_fused_kernel (+ l2_topk_kernel for ties)" if K <= 128 else "l2_dist_staged_kernel + l2_sort_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo},
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo, "traffic": traffic,
+                         "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch of "
+                                            "tools/scripts/l2_bench.py (1.25M reads x 128 random labels)")
+                         if traffic is not None else None},
             "window_table_embed_s": round(table_s, 2),
             "truth_top1": round(float(np.mean(ids[:, 0].astype(np.int64) == truth)), 4),
             "note": "post_process_l2_static on this step's neighbours (the reference's live rerank, whose outputs "
