@@ -273,7 +273,7 @@ def encoder_timing(d_q, Q, q_stride, dev, reps=3):
             "note": "Vectorizer::vectorize on the GPU; not inside `value` (the north star's path starts at embeddings)"}
 
 
-def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
+def l2_timing(table, d_I, d_x, d_q, q_stride, gru_queries, Q, K, truth, dev, reps=3):
     """The reference's live post-processing, post_process_l2_static (src/main.cpp:330), on this step's
     neighbours: drm_refs_embed builds the window-embedding table once (GRU, on the GPU), then
     drm_post_process_l2_static_device (l2_rerank.hip) is timed with HIP events. Algorithmic bytes per launch:
@@ -289,6 +289,11 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     t0 = time.time()
     embed_windows(table, enc, st)
     table_s = time.time() - t0
+    if not gru_queries:  # the table is the GRU's, so the query side must be too (the search ran on the stand-in)
+        d_l = DeviceBuffer.from_host(np.full(Q, q_stride, dtype=np.int32))
+        d_x = DeviceBuffer((Q, 128), np.float32)
+        enc.vectorize_device(d_q, d_l, Q, q_stride, d_x, st)
+        st.synchronize()
     enc.free()
     d_d, d_i, d_s = DeviceBuffer((Q, K), np.float32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
 
@@ -314,7 +319,7 @@ def l2_timing(table, d_I, d_x, Q, K, truth, dev, reps=3):
     gbs = algo / (ms * 1e-3) / 1e9
     # HBM bytes per dispatch from the committed PMC of tools/scripts/l2_bench.py (same Q and K, random labels)
     prof_path, pmc = committed_pmc("l2_fused_kernel" if K <= 128 else "l2_dist_staged_kernel", "l2_c5shape")
-    traffic = float(pmc["hbm_bytes_est"]) if pmc and "hbm_bytes_est" in pmc else None
+    traffic = float(pmc["hbm_bytes_est"]) if pmc and "hbm_bytes_est" in pmc and (Q, K) == (1_250_000, 128) else None
     return {"kernel": "l2_fused_kernel (+ l2_topk_kernel for ties)" if K <= 128 else "l2_dist_staged_kernel + l2_sort_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": algo, "traffic": traffic,
@@ -648,7 +653,8 @@ def main():
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
-    l2 = None if (args.no_l2 or flat) else l2_timing(table, d_I, d_x, Q, K, truth, dev)
+    l2 = None if (args.no_l2 or flat) else l2_timing(table, d_I, d_x, d_q, queries.shape[1], args.embed == "gru", Q, K,
+                                                         truth, dev)
 
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
