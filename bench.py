@@ -369,6 +369,10 @@ def gather_results(D, dev, n_total, bufs, local_host):
     way."""
     if D.world == 1:
         return None
+    from deepreadmapper_amd.device import device_count
+    ndev = device_count()
+    if D.world > ndev:  # RCCL needs one GPU per rank (drm_comm_init: DRM_ERR_UNSUPPORTED)
+        return {"skipped": f"{D.world} ranks share {ndev} device(s): the RCCL gather needs one GPU per rank"}
     try:
         from deepreadmapper_amd.device import DeviceBuffer, synchronize
         from deepreadmapper_amd.executor import Comm

@@ -40,6 +40,7 @@ EXPORTS = [
     "drm_vectorize", "drm_vectorize_device", "drm_encoder_flags",
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
     "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
+    "drm_index_set_search_waves", "drm_refs_set_sw_waves",
 ]
 
 
@@ -107,6 +108,8 @@ def lib():
         "drm_index_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
         "drm_index_free": (C.c_int, [vp]),
         "drm_index_get_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
+        "drm_index_set_search_waves": (C.c_int, [vp, i32]),
+        "drm_refs_set_sw_waves": (C.c_int, [vp, i32]),
         "drm_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "drm_search_device_ex": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),

@@ -323,6 +323,17 @@ int drm_search_fallbacks(drm_index *index, int64_t *count)
     });
 }
 
+int drm_index_set_search_waves(drm_index *index, int32_t waves_per_cu)
+{
+    return guarded([&] {
+        if (!index || waves_per_cu < 0)
+            throw Error(DRM_ERR_ARG, "invalid argument");
+        // the per-slot workspace was reserved at load for index->dev.waves_per_cu; more slots grow it on
+        // the next search, fewer use a prefix of it
+        index->dev.waves_per_cu = waves_per_cu > 0 ? waves_per_cu : 20;
+    });
+}
+
 int drm_index_get_info(const drm_index *index, drm_index_info *info)
 {
     return guarded([&] {
@@ -751,6 +762,15 @@ int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, in
     });
 }
 
+int drm_refs_set_sw_waves(drm_refs *refs, int32_t waves_per_cu)
+{
+    return guarded([&] {
+        if (!refs || waves_per_cu < 0)
+            throw Error(DRM_ERR_ARG, "invalid argument");
+        refs->dev.sw_waves_per_cu = waves_per_cu;
+    });
+}
+
 int drm_refs_free(drm_refs *refs)
 {
     return guarded([&] {
@@ -1080,9 +1100,19 @@ int drm_refs_embed(drm_refs *refs, drm_encoder *enc, void *stream)
             DRM_HIP_CHECK(hipFree(refs->dev.emb));
             refs->dev.emb = nullptr;
         }
-        if (!refs->dev.emb)
-            DRM_HIP_CHECK(drm::malloc_big((void **)&refs->dev.emb, sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d,
-                                          drm::kBigWindows));
+        if (!refs->dev.emb) {
+            // n x 512 B: a genome handle embeds one row per base (a 3 Gbp genome would need ~1.5 TB), so the table
+            // is checked against the device's free memory before it is asked for
+            const size_t bytes = sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d;
+            size_t free_b = 0, total_b = 0;
+            DRM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            if (bytes > free_b)
+                throw Error(DRM_ERR_UNSUPPORTED,
+                            "window-embedding table of " + std::to_string(n) + " rows needs " +
+                                std::to_string(bytes >> 30) + " GiB of device memory, " + std::to_string(free_b >> 30) +
+                                " GiB are free (a genome handle embeds one window per base)");
+            DRM_HIP_CHECK(drm::malloc_big((void **)&refs->dev.emb, bytes, drm::kBigWindows));
+        }
         refs->dev.emb_dim = (int32_t)d;
         refs->dev.emb_rows = n;
         const int64_t chunk = std::min<int64_t>(std::max<int64_t>(n, 1), (int64_t)4 << 20);

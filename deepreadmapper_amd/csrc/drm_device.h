@@ -219,6 +219,7 @@ struct DeviceRefs {
     int32_t *ws_scores = nullptr;
     int32_t *ws_ncand = nullptr;
     size_t ws_elems = 0, ws_nq = 0;
+    int32_t sw_waves_per_cu = 0; // > 0: SW score grid capped at this many waves per CU (co-resident search)
     // dynamic lookup (use_dynamic, post_process_sw_dynamic): the genome string instead of a window
     // table; window id w is genome[w / 2 ..+ ref_len), reverse-complemented when w is odd
     uint8_t *genome = nullptr;

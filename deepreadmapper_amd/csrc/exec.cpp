@@ -649,7 +649,14 @@ int drm_comm_init(const uint8_t *id, int nranks, int rank, int device, drm_comm 
         std::unique_ptr<drm_comm> c(new drm_comm());
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        nccl_check(ncclCommInitRank(&c->comm, nranks, u, rank), "ncclCommInitRank");
+        const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+        // RCCL needs one GPU per rank: ranks that share a device (a rehearsal of N ranks on fewer GPUs) are
+        // refused by it as "invalid usage"; say what it means instead
+        if (r == ncclInvalidUsage)
+            throw Error(DRM_ERR_UNSUPPORTED, "ncclCommInitRank: invalid usage -- RCCL needs one GPU per rank, and "
+                                             "rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                             " shares device " + std::to_string(device) + " with another rank");
+        nccl_check(r, "ncclCommInitRank");
         c->nranks = nranks;
         c->rank = rank;
         c->device = device;

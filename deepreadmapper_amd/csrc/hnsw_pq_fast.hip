@@ -331,9 +331,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     } while (0)
 
 // LOGRES: k == ef (result set from the log); else k <= 64 (register result set).
-// FIX128: k = ef = efSearch = 128 and no repeated links (the pipeline's EF = K = 128 on a clean
-// index) as compile-time constants: fewer live SGPRs (no spills to VGPR lanes, no kernel-argument
-// reloads inside the hop loop) and no duplicate-link pass.
+// FIX128: ef = efSearch = 128 (and k = 128 with LOGRES) and no repeated links as compile-time constants:
+// the pipeline's EF = K = 128 on a clean index, and the sparse default k_clusters = 5 at EF = 128
+// (src/main.cpp:56-63,278) -- fewer live SGPRs (no spills to VGPR lanes, no kernel-argument reloads
+// inside the hop loop) and no duplicate-link pass.
 template <bool LOGRES, bool STAMPS, bool FIX128>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
 {
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
-    const int ef = FIX128 ? 128 : a.ef, k = FIX128 ? 128 : a.k, deg0 = a.deg0;
+    const int ef = FIX128 ? 128 : a.ef, k = (FIX128 && LOGRES) ? 128 : a.k, deg0 = a.deg0;
     const int ef_search = FIX128 ? 128 : a.efSearch;
     const bool check_dups = FIX128 ? false : (a.check_dups != 0);
     const PathConst pconst(lane);
@@ -657,9 +658,11 @@ bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream)
 {
     const bool logres = a.k == a.ef;
-    const bool fix = logres && a.k == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
-    if (fix)
+    const bool fix = a.ef == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
+    if (fix && logres)
         hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (fix)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true>), dim3(slots), dim3(64), lds, stream, a);
     else if (logres) {
         if (stamps)
             hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false>), dim3(slots), dim3(64), lds, stream, a);

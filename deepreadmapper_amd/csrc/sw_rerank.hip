@@ -65,7 +65,7 @@ struct CandRow {
 // Dynamic (:72-201): dense keeps every id (out-of-genome windows are empty); the sparse expansion is
 // checked against the genome length. Duplicates are kept (the mapping restores the original count).
 template <typename T>
-__device__ int find_candidates(const RerankArgs &a, const int64_t *nb, int nsel, T *cand)
+__device__ int find_candidates(const RerankArgs &a, const int64_t *nb, int nsel, T *cand, int cap = kMaxCands)
 {
     const uint64_t limit = a.genome ? (uint64_t)a.glen : (uint64_t)a.n_ref;
     int nc = 0;
@@ -73,7 +73,7 @@ __device__ int find_candidates(const RerankArgs &a, const int64_t *nb, int nsel,
         const uint64_t id = (uint64_t)nb[i];
         if (a.stride == 1) {
             if (a.genome || id < limit) {
-                if (nc >= kMaxCands)
+                if (nc >= cap)
                     return -2;
                 cand[nc++] = a.genome ? (T)(id < (uint64_t)kNoWindow ? id : kNoWindow) : (T)id;
             }
@@ -86,7 +86,7 @@ __device__ int find_candidates(const RerankArgs &a, const int64_t *nb, int nsel,
         const uint64_t start = (actual >= s - 1) ? actual - s + 1 : 0;
         const uint64_t end = min(actual + s, limit);
         for (uint64_t pos = start; pos < end; ++pos) {
-            if (nc >= kMaxCands)
+            if (nc >= cap)
                 return -2;
             cand[nc++] = (T)pos;
         }
@@ -415,10 +415,14 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
     constexpr int PST = ((LQ + 3) & ~3) + 4 + (((((LQ + 3) & ~3) + 4) / 4) % 2 == 0 ? 4 : 0);
     constexpr int GST = 5 * PST + 4 * (((4 - 5 * (PST / 4)) % 16 + 16) % 16);
     static_assert((PST / 4) % 2 == 1 && (GST / 4) % 16 == 4, "pair-profile bank spread");
-    __shared__ __align__(16) uint32_t pprof[5 * GST];
+    // the last ka block needs only its 5 rows, not a full GST: with the candidate list sized to the call
+    // (dynamic LDS, a.cmax entries) a 152-byte query's workgroup fits 16 KB, so one SW wave per SIMD can sit
+    // beside three search waves (8 KB of LUT each) on a CU (co-resident search + rerank)
+    constexpr int PPROF = 4 * GST + 5 * PST;
+    __shared__ __align__(16) uint32_t pprof[PPROF];
     __shared__ __align__(16) uint8_t qbuf[(LQ + 15) & ~15];
     __shared__ uint32_t qmask[8]; // bytes present in the query
-    __shared__ uint32_t cand[kMaxCands];
+    extern __shared__ uint32_t cand[]; // [a.cmax]
     __shared__ int ncand_s, flag_s;
 
     const int tid = threadIdx.x; // one wave per workgroup
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 ncand_s = base;
         } else if (tid == 0) {
             // sparse (:238-335) or dynamic lookup: expand, duplicates kept (:502-507)
-            ncand_s = find_candidates(a, nb, nsel, cand);
+            ncand_s = find_candidates(a, nb, nsel, cand, a.cmax);
         }
         for (int t = tid; t < ((LQ + 15) & ~15); t += 64)
             qbuf[t] = (t < qlen && t < LQ) ? a.queries[q * a.q_stride + t] : 0;
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         __syncthreads();
         for (int t = tid; t < qlen && t < LQ; t += 64)
             atomicOr(&qmask[qbuf[t] >> 5], 1u << (qbuf[t] & 31));
-        for (int e = tid; e < 5 * GST; e += 64) {
+        for (int e = tid; e < PPROF; e += 64) {
             const int ka = e / GST, kb = (e % GST) / PST, j = (e % GST) % PST;
             uint32_t word = 0;
             if (kb < 5 && j < qlen && j < LQ) {
@@ -687,7 +691,17 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     a.cand_ids = refs.ws_ids;
     a.cand_scores = refs.ws_scores;
     a.ncand = refs.ws_ncand;
-    const int grid = (int)std::min<int64_t>(a.nq, 65536);
+    // One one-wave workgroup per query up to 65536 (grid-stride beyond). refs.sw_waves_per_cu > 0 caps the
+    // grid at that many resident waves per CU instead, leaving the rest of every CU to a search kernel
+    // running beside the rerank on another stream (drm_refs_set_sw_waves).
+    int64_t gcap = 65536;
+    if (refs.sw_waves_per_cu > 0) {
+        int cus = 0;
+        DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, refs.device));
+        gcap = (int64_t)std::max(cus, 1) * refs.sw_waves_per_cu;
+    }
+    const int grid = (int)std::min<int64_t>(a.nq, gcap);
+    const size_t cand_lds = sizeof(uint32_t) * (size_t)cmax; // sw_score_f16_kernel's candidate list
     // fp16 pair-profile kernel for queries up to 152 bytes; the bit-profile kernel re-scores the
     // queries it flagged, and takes longer queries (or everything when DRM_SW_BITPROFILE=1).
     static const bool force_bits = [] {
@@ -699,7 +713,7 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         if (force_bits) {
             hipLaunchKernelGGL((sw_score_kernel<64>), dim3(grid), dim3(64), 0, stream, a);
         } else {
-            hipLaunchKernelGGL((sw_score_f16_kernel<64>), dim3(grid), dim3(64), 0, stream, a);
+            hipLaunchKernelGGL((sw_score_f16_kernel<64>), dim3(grid), dim3(64), cand_lds, stream, a);
             hipLaunchKernelGGL((sw_score_kernel<64, true>), dim3(grid), dim3(64), 0, stream, a);
         }
         break;
@@ -707,7 +721,7 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         if (force_bits) {
             hipLaunchKernelGGL((sw_score_kernel<152>), dim3(grid), dim3(64), 0, stream, a);
         } else {
-            hipLaunchKernelGGL((sw_score_f16_kernel<152>), dim3(grid), dim3(64), 0, stream, a);
+            hipLaunchKernelGGL((sw_score_f16_kernel<152>), dim3(grid), dim3(64), cand_lds, stream, a);
             hipLaunchKernelGGL((sw_score_kernel<152, true>), dim3(grid), dim3(64), 0, stream, a);
         }
         break;

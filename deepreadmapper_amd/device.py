@@ -50,22 +50,6 @@ class DeviceBuffer:
             check(lib().drm_memcpy_d2h(ptr(out), self.ptr, self.nbytes))
         return out
 
-    @property
-    def __cuda_array_interface__(self):
-        """Zero-copy view for torch.as_tensor (used for the RCCL result gather, never for compute)."""
-        return {"shape": self.shape, "typestr": self.dtype.str, "data": (self.ptr, False), "version": 2}
-
-    def byte_rows(self):
-        """The buffer as [shape[0], row_bytes] uint8 (same memory), for dtype-agnostic collectives."""
-        rows = self.shape[0] if self.shape else 1
-        width = self.nbytes // max(rows, 1)
-        parent = self
-
-        class _View:
-            __cuda_array_interface__ = {"shape": (rows, width), "typestr": "|u1", "data": (parent.ptr, False),
-                                        "version": 2}
-        return _View()
-
     def zero(self):
         check(lib().drm_memset(self.ptr, 0, max(self.nbytes, 1)))
 

@@ -1,8 +1,8 @@
 """Multi-GPU sharding of the query batch: every query is independent, so the
 index is replicated on each GPU and queries are split into contiguous ranges; the only exchange is
 gathering fixed-size per-rank results to rank 0 for output (indices/distances/SW scores), off the
-hot path. Backend: whatever torch.distributed group the caller initialised (gloo on CPU, nccl =
-RCCL over xGMI on GPUs)."""
+hot path. gather_rows is the host-side form over a torch.distributed group (gloo: the CPU tests);
+device-resident rows go over RCCL from C++ (drm_comm_gather_rows, executor.Comm)."""
 import numpy as np
 
 
@@ -36,30 +36,3 @@ def gather_rows(arr, n_total, rank, world, dist):
         parts.append(outs[r].numpy()[: h - l])
     full = np.concatenate(parts, axis=0)
     return full.view(a.dtype).reshape((n_total,) + a.shape[1:])
-
-
-def gather_rows_device(buf, n_total, rank, world, dist, group=None):
-    """RCCL (nccl-backend) version of gather_rows for device-resident results: `buf` is a
-    DeviceBuffer holding this rank's rows [lo:hi) of an [n_total, ...] result. Every rank's block is
-    padded to the largest shard and all-gathered over xGMI; rank 0 returns the full array on the host
-    (numpy), other ranks None."""
-    import torch
-    lo, hi = shard_range(n_total, rank, world)
-    rows = max(shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0] for r in range(world))
-    assert buf.shape[0] == hi - lo
-    dev = torch.device("cuda", torch.cuda.current_device())
-    mine = torch.as_tensor(buf.byte_rows(), device=dev)
-    width = mine.shape[1]
-    send = torch.zeros((rows, width), dtype=torch.uint8, device=dev)
-    send[: mine.shape[0]].copy_(mine)
-    out = torch.empty((world * rows, width), dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(out, send, group=group)
-    if rank != 0:
-        return None
-    host = out.cpu().numpy()
-    parts = []
-    for r in range(world):
-        l, h = shard_range(n_total, r, world)
-        parts.append(host[r * rows: r * rows + (h - l)])
-    full = np.ascontiguousarray(np.concatenate(parts, axis=0))
-    return full.view(buf.dtype).reshape((n_total,) + tuple(buf.shape[1:]))

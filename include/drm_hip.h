@@ -103,6 +103,11 @@ int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, 
  * contained in nhops (they read M_hnsw-wide rows instead of 2*M_hnsw-wide ones). */
 int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                          int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, void *stream);
+/* Tuning (no reference counterpart): resident search waves per CU of this index's persistent search grid
+ * (0 = the default, 20: every CU's LDS holds 20 PQ lookup tables of 8 KB). Fewer leave room on every CU
+ * for a rerank kernel running beside the search on another stream (drm_refs_set_sw_waves). Results do
+ * not depend on it. */
+int drm_index_set_search_waves(drm_index *index, int32_t waves_per_cu);
 /* Diagnostic (no reference counterpart): how many queries of the last search on this index met an
  * exact distance tie and were re-run by the exact (faiss heap-layout) kernel. Synchronizes the device. */
 int drm_search_fallbacks(drm_index *index, int64_t *count);
@@ -168,6 +173,10 @@ int drm_refs_is_genome(const drm_refs *refs, int *is_genome);
  * and only A/C/G/T/N kept (from every later line, headers included -- the reference's behaviour).
  * Two calls: *len receives the length (out may be NULL), then out[0 .. *len) the sequence. */
 int drm_extract_fasta_sequence(const char *path, uint8_t *out, int64_t *len);
+/* Tuning (no reference counterpart): cap the SW score kernel's grid at waves_per_cu resident waves per CU
+ * (0 = uncapped: one wave per query up to 65536). Used to run the rerank of one batch beside the search of
+ * the next on the same CUs (drm_index_set_search_waves). Results do not depend on it. */
+int drm_refs_set_sw_waves(drm_refs *refs, int32_t waves_per_cu);
 /* Shape and device of a window table (any out-pointer may be NULL). */
 int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device);
 

@@ -112,3 +112,38 @@ def test_gpu_build_c3_scale(tmp_path):
         rec[name] = float(np.mean((I == w.truth[:, None]).any(axis=1)))
     print(f"C3 GPU build {t_gpu:.1f}s (incl. embedding + file write); recall {rec}")
     assert rec["gpu"] >= 0.9 * rec["host"]
+
+
+def test_hnswpq_index_cli_builds_c3_on_gpu(tmp_path):
+    """The drop-in `hnswpq_index` CLI (src/hnswpq/index.cpp:195-316) builds C3 (a 500,149 bp genome, 1M
+    windows) with the GPU builder when a GPU is present (DRM_BUILD_DEVICE=gpu forces it here), writing the
+    same config.txt + prefix/prefix.index the reference writes, and bin/pipeline reads that index: its
+    indices.npy / distances.npy on 2,000 reads equal the oracle's search of the same file."""
+    import subprocess
+    from deepreadmapper_amd import synth
+    from oracle import faiss_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = synth.genome(500_149, seed=42)
+    synth.write_fasta(str(tmp_path / "c3.fna"), g)
+    reads, names, _ = synth.simulate_reads(g, 2000, seed=7)
+    synth.write_fastq(str(tmp_path / "c3.fastq"), reads, names)
+    env = {k: v for k, v in os.environ.items() if k != "DRM_ENCODER"}
+    env["DRM_BUILD_DEVICE"] = "gpu"
+    t0 = time.time()
+    r = subprocess.run([os.path.join(root, "bin", "hnswpq_index"), "c3.fna", "c3g", "150"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "graph built on GPU" in r.stdout
+    print(f"hnswpq_index C3 on the GPU: {time.time() - t0:.1f}s")
+    cfg = dict(l.split(": ", 1) for l in open(tmp_path / "c3g" / "config.txt").read().splitlines())
+    assert cfg["n_vects"] == "1000000" and cfg["stride"] == "1" and cfg["index_file"] == "c3g/c3g.index"
+    fx = faiss_file.read(str(tmp_path / "c3g" / "c3g.index"))
+    assert fx.ntotal == 1_000_000
+    r = subprocess.run([os.path.join(root, "bin", "pipeline"), "c3g", "c3.fastq", "c3.fna", "128", "128", "128", "out"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    I = np.load(tmp_path / "out" / "indices.npy")
+    D = np.load(tmp_path / "out" / "distances.npy")
+    Do, Io, _, _ = O.hnswpq_search(fx, synth.embed(synth.tag(reads)), 128, 128,
+                                   nthreads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    assert np.array_equal(I.astype(np.int64), Io) and np.array_equal(D.view(np.uint32), Do.view(np.uint32))

@@ -82,3 +82,46 @@ def test_c5_l2_rerank_vs_oracle(c5):
     assert np.array_equal(d.view(np.uint32), wd.view(np.uint32))
     assert np.array_equal(ids, uniq[wi.astype(np.int64)].astype(np.uint64))
     table.free()
+
+
+def test_c5_full_slice_properties(c5):
+    """The bench's whole per-GPU slice (1,250,000 reads of the same seeded stream, GRU-embedded): device
+    search + device SW rerank at EF = K = 128 over every read, with the size-independent checks on every
+    row -- ascending search rows, labels inside the table, ndis / nhops > 0, status == K, SW scores
+    descending and within [0, 150], each row's SW ids a permutation of its search ids (dense, all 128 ids
+    valid: find_sequences keeps them all, post_processor.cpp:215-236) -- and the first 512 rows equal to
+    the oracle-checked sample above (reads [0, 512) of the stream)."""
+    from deepreadmapper_amd import read_index, synth, WindowTable
+    from deepreadmapper_amd.device import DeviceBuffer, synchronize
+    from deepreadmapper_amd._native import check, lib
+    K = EF = 128
+    Q = 1_250_000
+    g = synth.genome(C5_GENOME, seed=44)
+    reads, truth = synth.simulate_reads_range(g, 0, Q, seed=9)
+    q = synth.tag(reads)
+    x = synth.embed_gru(q)
+    assert np.array_equal(x[:SAMPLE], c5["x"])
+    ix = read_index(c5["index"])
+    table = WindowTable(c5["refs"])
+    d_x, d_q = DeviceBuffer.from_host(x), DeviceBuffer.from_host(q)
+    d_ql = DeviceBuffer.from_host(np.full(Q, q.shape[1], dtype=np.int32))
+    d_D, d_I = DeviceBuffer((Q, K), np.float32), DeviceBuffer((Q, K), np.int64)
+    nd, nh = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
+    d_sc, d_id, d_st = DeviceBuffer((Q, K), np.int32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
+    ix.search_device(d_x, Q, K, EF, d_D, d_I, nd, nh)
+    check(lib().drm_post_process_sw_static_device(table.handle, d_I.ptr, Q, K, d_q.ptr, d_ql.ptr, q.shape[1], 1, K, K,
+                                                  d_sc.ptr, d_id.ptr, d_st.ptr, None))
+    synchronize()
+    D, I = d_D.download(), d_I.download()
+    assert (np.diff(D, axis=1) >= 0).all()
+    assert (I >= 0).all() and (I < len(c5["refs"])).all()
+    assert (nd.download() > 0).all() and (nh.download() > 0).all()
+    st, sc, ids = d_st.download(), d_sc.download(), d_id.download()
+    assert (st == K).all()
+    assert (np.diff(sc, axis=1) <= 0).all() and (sc >= 0).all() and (sc <= 150).all()
+    assert np.array_equal(np.sort(ids.astype(np.int64), axis=1), np.sort(I, axis=1))
+    D0, I0, _ = ix.search(c5["x"], K, EF)
+    assert np.array_equal(I[:SAMPLE], I0) and np.array_equal(D[:SAMPLE].view(np.uint32), D0.view(np.uint32))
+    assert float(np.mean(ids[:, 0].astype(np.int64) == truth)) > 0.6
+    table.free()
+    ix.free()

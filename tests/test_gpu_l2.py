@@ -243,12 +243,14 @@ def test_l2_dynamic_errors(enc, genome_table):
     assert e.value.code == DRM_ERR_ARG and "Invalid mapping index" in str(e.value)
 
 
-def test_pipeline_cli_dynamic_sparse_sam_is_l2(tmp_path):
-    """bin/pipeline use_dynamic=1 use_streaming=1 on a stride-2 index with the GRU model: the SAM rows come from
-    post_process_l2_dynamic_streaming's L2 rerank. Sparse labels run to ~2 * genome length / stride while the
-    expansion keeps only label * stride < genome length, so about half of them expand to nothing; the stream is
-    then shorter than the reference's query boundaries and the reference reads past its arrays for the tail
-    queries. The CLI stops with the reference's error message instead."""
+def test_pipeline_cli_dynamic_sparse_sam(tmp_path):
+    """bin/pipeline use_dynamic=1 use_streaming=1 on a stride-2 index with the GRU model.
+    Default: the reference's observable output, a header-only SAM -- its sparse-branch write_sam_streaming
+    call (src/utils/post_processor.cpp:1004-1005) leaves batch_query_count at its default 0
+    (includes/utils/utils.hpp:99), so no row is written. DRM_SAM_L2_ROWS=1: the L2 rerank's rows. Sparse labels
+    run to ~2 * genome length / stride while the expansion keeps only label * stride < genome length, so the
+    stream is shorter than the reference's query boundaries and the tail queries' ranges run past it (the
+    reference reads out of bounds there): those queries are written without rows, the run still succeeds."""
     import os
     import subprocess
     from deepreadmapper_amd.encoder import DEFAULT_MODEL
@@ -260,9 +262,22 @@ def test_pipeline_cli_dynamic_sparse_sam_is_l2(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     # ef 128, k 10, k_clusters 64 (src/main.cpp:54-62): 64 labels x 3 windows of boundary per query
-    r = subprocess.run([os.path.join(root, "bin", "pipeline"), "s2", fq, fna, "128", "10", "64", "out", "1", "1"],
-                       cwd=tmp_path, env=env, capture_output=True, text=True)
-    assert r.returncode == 1 and "Invalid mapping index" in r.stderr, r.stdout + r.stderr
+    argv = [os.path.join(root, "bin", "pipeline"), "s2", fq, fna, "128", "10", "64", "out", "1", "1"]
+    r = subprocess.run(argv, cwd=tmp_path, env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    sam = open(tmp_path / "out" / "results.sam").read()
+    assert sam == "@HD\tVN:1.0\tSO:unsorted\n@SQ\tSN:ref\tLN:150\n"
+    r = subprocess.run(argv, cwd=tmp_path, env=dict(env, DRM_SAM_L2_ROWS="1"), capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "clipped expansion stream" in r.stdout
+    lines = open(tmp_path / "out" / "results.sam").read().splitlines()
+    rows = [l.split("\t") for l in lines[2:]]
+    assert lines[:2] == ["@HD\tVN:1.0\tSO:unsorted", "@SQ\tSN:ref\tLN:150"] and len(rows) > 0
+    per_q = {}
+    for f in rows:
+        per_q[f[0]] = per_q.get(f[0], 0) + 1
+        assert f[2] == "ref" and f[4] == "60" and f[5] == "150M" and 1 <= int(f[3]) <= 1000
+    assert all(c == 10 for c in per_q.values()) and len(per_q) < 150
 
 
 def test_post_process_l2_dynamic_reference_shape(enc, genome_table):

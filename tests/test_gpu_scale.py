@@ -2,8 +2,10 @@
 
 * C3 -- synthetic 1M x 150 bp dense windows, 100k reads: the live-path IndexHNSWPQ (M_hnsw 16,
   EFC 200, PQ 8x8) and the hnswlib fp32 index (M 64, EFC 128), both built here on the box.
-* C4r -- C4's sparse shape (stride 4, PQ 8x8, M_hnsw 16) at a reduced N: 2M windows of a 4 Mbp
-  genome (the full 10M build does not fit a test window on the CPU builder), K = 128 and K = 5.
+* C4 -- BASELINE configs[3] at its configured size: a seeded 20,000,299 bp genome, stride-4 sparse
+  IndexHNSWPQ of 10,000,000 windows (PQ 8x8, M_hnsw 16, EFC 200) built on the GPU (builder_gpu.hip,
+  seconds), 1,000,000 reads, K = 128 and the reference's sparse default k_clusters = K = 5
+  (src/main.cpp:56-63,278), and the sparse SW rerank (post_process_sw_static at stride 4).
 
 On each: the HIP search + SW rerank on a fixed query sample equal the oracle bit for bit (ids,
 0-ulp distances, ndis / nhops, SW scores and their partial_sort order), and every query of the
@@ -37,12 +39,14 @@ def c3():
 
 
 @pytest.fixture(scope="module")
-def c4r():
+def c4():
     from deepreadmapper_amd import synth
     from oracle import faiss_file
-    w = synth.Workload("c4r", 4_000_299, 50_000, stride=4, seed=43, read_seed=8).generate(
-        CACHE, nthreads=_threads(), need_refs=False)
-    return {"w": w, "fx": faiss_file.read(w.index_path)}
+    w = synth.Workload("c4", 20_000_299, 1_000_000, stride=4, seed=43, read_seed=8).generate(
+        CACHE, need_refs=False, gpu_build=True)
+    fx = faiss_file.read(w.index_path)
+    assert fx.ntotal == 10_000_000
+    return {"w": w, "fx": fx}
 
 
 def _sample(n):
@@ -137,18 +141,24 @@ def test_c3_flat_search_sample(c3):
 
 
 @pytest.mark.parametrize("k", [128, 5])
-def test_c4r_sparse_pq_search(c4r, k):
-    w = c4r["w"]
-    _check_search(w.index_path, c4r["fx"], w.q_emb, k, 128, c4r["fx"].ntotal)
+def test_c4_sparse_pq_search(c4, k):
+    """All 1M C4 queries through the device search (property checks), a 2,000-query sample bit-exact
+    against the oracle (ids, 0-ulp distances, ndis, nhops); src/hnswpq/index.cpp:215,270 (stride 4),
+    src/main.cpp:278 (search k = k_clusters)."""
+    w = c4["w"]
+    _check_search(w.index_path, c4["fx"], w.q_emb, k, 128, c4["fx"].ntotal)
 
 
-def test_c4r_sparse_rerank(c4r):
-    """post_process_sw_static on the stride-4 index: the reference's sparse defaults (k_clusters = 5,
-    K = 5) and K = 128 over k_clusters = 20 (K <= k_clusters * 2 * stride, post_processor.cpp:486-489,
-    and 20 ids expand to 140 >= K windows, reranker.cpp:26-29)."""
+def test_c4_sparse_rerank(c4):
+    """post_process_sw_static on the stride-4 10M-window index over the stride-1 window table of the same
+    genome (src/utils/post_processor.cpp:238-335): the reference's sparse defaults (k_clusters = 5, K = 5)
+    and K = 128 over k_clusters = 20 (K <= k_clusters * 2 * stride, post_processor.cpp:486-489, and 20 ids
+    expand to up to 140 >= K windows, reranker.cpp:26-29), 20,000 reads, a 2,000-read sample against the
+    oracle."""
     from deepreadmapper_amd import synth
-    w = c4r["w"]
+    w = c4["w"]
     refs = synth.windows_lookup(w.genome, 150, 1)
+    assert len(refs) == 2 * (20_000_299 - 149)
     for k, kc in ((5, 5), (128, 20)):
         _, I, _, _ = _search_full(w.index_path, w.q_emb[:20_000], kc, 128)
         _check_rerank(refs, I, w.queries[:20_000], 4, k, kc)

@@ -5,8 +5,13 @@
 // <index_prefix>/<index_prefix>.index (:212) in faiss IndexHNSWPQ format.
 // Sequence inputs are read as tagged windows (read_file(ref, ref_len, stride), :270) and embedded
 // by the GRU model on the GPU (DRM_ENCODER, or the reference's models/ path in the working directory,
-// :279-280) or else the deterministic 3-mer stand-in. Extra knobs via env: DRM_BUILD_THREADS (default:
-// all cores), DRM_BUILD_SEED (default 0), DRM_DEVICE (encoder GPU).
+// :279-280) or else the deterministic 3-mer stand-in.
+// The graph (build_faiss_index, :86-193) is built on the GPU (drm_build_hnswpq_device, builder_gpu.hip:
+// 50M windows in about half a minute) when a GPU is present and the shape is the one it supports (d = 128,
+// M_pq = 8, nbits = 8, M_hnsw <= 32), else by the host builder (drm_build_hnswpq, OpenMP like the
+// reference's omp_set_num_threads(128) at :116). Extra knobs via env: DRM_BUILD_DEVICE (auto | gpu | cpu),
+// DRM_BUILD_THREADS (host builder threads, default: all cores), DRM_BUILD_SEED (default 0), DRM_DEVICE
+// (the GPU for the encoder and the builder).
 #include <cstdlib>
 #include <cstring>
 #include <filesystem>
@@ -96,7 +101,39 @@ int main(int argc, char *argv[])
         };
         drm::save_config(config, prefix);
         std::filesystem::create_directories(prefix);
-        drm::build_hnswpq(emb.data(), (int64_t)n, (int)dim, M_pq, nbits, M_hnsw, EFC, 0.5, threads, seed, index_file);
+        const std::string mode = std::getenv("DRM_BUILD_DEVICE") ? std::getenv("DRM_BUILD_DEVICE") : "auto";
+        if (mode != "auto" && mode != "gpu" && mode != "cpu")
+            throw drm::Error(DRM_ERR_ARG, "DRM_BUILD_DEVICE must be auto, gpu or cpu");
+        int ndev = 0;
+        if (mode != "cpu" && drm_device_count(&ndev) != DRM_OK)
+            ndev = 0;
+        const bool gpu_shape = dim == 128 && M_pq == 8 && nbits == 8 && M_hnsw >= 2 && M_hnsw <= 32;
+        if (mode == "gpu" && (ndev < 1 || !gpu_shape))
+            throw drm::Error(DRM_ERR_UNSUPPORTED, ndev < 1 ? "DRM_BUILD_DEVICE=gpu but no GPU is visible"
+                                                           : "the GPU builder supports d = 128, M_pq = 8, nbits = 8, "
+                                                             "M_hnsw <= 32");
+        if (mode != "cpu" && ndev >= 1 && gpu_shape) {
+            const int device = std::getenv("DRM_DEVICE") ? std::atoi(std::getenv("DRM_DEVICE")) : 0;
+            void *d_x = nullptr;
+            auto chk = [](int rc) {
+                if (rc != DRM_OK)
+                    throw drm::Error(rc, drm_last_error());
+            };
+            chk(drm_set_device(device));
+            chk(drm_malloc(&d_x, sizeof(float) * n * dim));
+            int rc = drm_memcpy_h2d(d_x, emb.data(), sizeof(float) * n * dim);
+            if (rc == DRM_OK)
+                rc = drm_build_hnswpq_device(static_cast<const float *>(d_x), (int64_t)n, (int32_t)dim, M_pq, nbits,
+                                             M_hnsw, EFC, 0.5, seed, device, index_file.c_str());
+            const std::string err = rc == DRM_OK ? "" : drm_last_error();
+            drm_free(d_x);
+            if (rc != DRM_OK)
+                throw drm::Error(rc, err);
+            std::cout << "[BUILD INDEX] graph built on GPU " << device << std::endl;
+        } else {
+            drm::build_hnswpq(emb.data(), (int64_t)n, (int)dim, M_pq, nbits, M_hnsw, EFC, 0.5, threads, seed,
+                              index_file);
+        }
         std::cout << "[BUILD INDEX] IndexHNSWPQ written to " << index_file << std::endl;
     } catch (const std::exception &e) {
         std::cerr << "Error: " << e.what() << std::endl;

@@ -268,12 +268,21 @@ int main(int argc, char *argv[])
         // the whole run by L2 (:884-1010): drm_post_process_l2_dynamic over every query after the search, on a
         // window-embedding table of the genome built by the GRU model. Without the model (3-mer stand-in) or
         // across several devices, those SAM rows come from the SW rerank instead.
+        //
+        // What the reference's sparse branch writes is only the SAM header: its write_sam_streaming call there
+        // (post_processor.cpp:1004-1005) leaves out batch_query_count, which defaults to 0
+        // (includes/utils/utils.hpp:99), so the row loop (utils.cpp:452) never runs. That header-only file is
+        // the default here too (no rerank is computed for it). DRM_SAM_L2_ROWS=1 opts into the rows the
+        // reranker meant to write: the L2 rows of every query, and none for a query whose
+        // candidate range runs past the clipped expansion stream (the reference reads out of bounds there).
         const bool stream_sam = use_streaming && dyn;
         const bool sam_from_search = stream_sam && stride == 1;
-        const bool sam_l2 = stream_sam && stride > 1 && rt && !is_npy && !drm::encoder_model_path().empty();
+        const bool l2_rows = std::getenv("DRM_SAM_L2_ROWS") && std::atoi(std::getenv("DRM_SAM_L2_ROWS")) != 0;
+        const bool sam_header_only = stream_sam && stride > 1 && !l2_rows;
+        const bool sam_l2 = stream_sam && stride > 1 && l2_rows && rt && !is_npy && !drm::encoder_model_path().empty();
         if (stream_sam && (size_t)k > (size_t)k_clusters * 2 * stride) // post_processor.cpp:769-772
             throw drm::Error(DRM_ERR_K, "Final k too large. Ensure k < k_clusters * 2 * stride to have enough candidates.");
-        if (stream_sam && stride > 1 && !sam_l2)
+        if (stream_sam && stride > 1 && l2_rows && !sam_l2)
             std::cout << "[MAIN] stride > 1 without the GRU model on one device: SAM rows from the SW rerank (the "
                          "reference reranks them by L2 here)"
                       << std::endl;
@@ -292,7 +301,13 @@ int main(int argc, char *argv[])
                                      sw_scores.p + lo * k, sw_ids.p + lo * k, status.p + lo, sp);
         };
         int rc = DRM_OK;
-        if (sam_l2) {
+        if (sam_header_only) {
+            std::cout << "[MAIN] Using STREAMING output to SAM file: " << sam_file << std::endl;
+            std::filesystem::create_directories(out_dir);
+            rc = run(0, nq, &st); // faiss_search of the whole run (src/main.cpp:278)
+            if (rc == DRM_OK)
+                drm::write_sam_block(sam_file, true, "ref", ref_len, qseqs, qids, 0, 0, nullptr, nullptr, (size_t)k);
+        } else if (sam_l2) {
             std::cout << "[MAIN] Using STREAMING output to SAM file: " << sam_file << std::endl;
             std::filesystem::create_directories(out_dir);
             rc = run(0, nq, &st);
@@ -307,8 +322,20 @@ int main(int argc, char *argv[])
                 std::vector<uint64_t> l2i(nq * (size_t)k);
                 std::vector<int32_t> cnt(nq);
                 int64_t bad = -1;
-                check(drm_post_process_l2_dynamic(rt, I.p, (int64_t)nq, k_clusters, x.p, (int32_t)dim, (int64_t)stride,
-                                                  k, k_clusters, l2d.data(), l2i.data(), cnt.data(), &bad));
+                const int lrc = drm_post_process_l2_dynamic(rt, I.p, (int64_t)nq, k_clusters, x.p, (int32_t)dim,
+                                                            (int64_t)stride, k, k_clusters, l2d.data(), l2i.data(),
+                                                            cnt.data(), &bad);
+                // a candidate range past the clipped stream (status -4): that query keeps no row, the others are
+                // written (every output was downloaded before the error was raised)
+                if (lrc == DRM_ERR_ARG && bad >= 0) {
+                    size_t clipped = 0;
+                    for (size_t i = 0; i < nq; ++i)
+                        clipped += cnt[i] == 0;
+                    std::cout << "[MAIN] " << clipped << " queries (first " << bad
+                              << ") rerank past the clipped expansion stream: written without rows" << std::endl;
+                } else {
+                    check(lrc);
+                }
                 std::cout << "[MAIN] L2 rerank (dynamic, stride " << stride << ") time: " << ms_since(tl) << " ms"
                           << std::endl;
                 size_t block = 1u << 20;
