@@ -509,6 +509,9 @@ def main():
     ap.add_argument("--no-host-path", action="store_true", help="skip the pinned-host drm_search_rerank timing")
     ap.add_argument("--no-encoder", action="store_true", help="skip the GRU read-encoder timing")
     ap.add_argument("--no-l2", action="store_true", help="skip the L2 rerank (post_process_l2_static) timing")
+    ap.add_argument("--co", action="store_true", help="co-scheduled step (drm_search_rerank_device: search(b) beside "
+                                                       "SW rerank(b-1) on the same CUs) instead of search all, then SW all; "
+                                                       "measured no faster at C5 (DESIGN.md sec. 5)")
     ap.add_argument("--embed", choices=["kmer3", "gru"], default=None,
                     help="embeddings of windows and reads: gru (default for c5: the reference's GRU model, run on the "
                          "GPU by drm_vectorize) or kmer3 (the deterministic 3-mer stand-in; default for c3/c4)")
@@ -578,8 +581,20 @@ def main():
     d_nd, d_nh, d_nu = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
     d_sc, d_id, d_st = DeviceBuffer((Q, K), np.int32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
     stream = Stream()
+    co = args.co and not flat
+    pstats = []
 
     def step(ev=None):
+        if co:
+            # drm_search_rerank_device: the search of batch b beside the SW rerank of batch b-1 on the same CUs
+            # (exec.cpp); stats = per-step device span and summed launch spans (the call synchronises)
+            from deepreadmapper_amd.executor import search_rerank_device
+            st = search_rerank_device(ix, table, d_x, Q, d_q, d_ql, queries.shape[1], d_D, d_I, d_sc, d_id, d_st, k=K,
+                                      ef=EF, d_ndis=d_nd, d_nhops=d_nh, d_nhops_upper=d_nu, stream=stream,
+                                      stats=ev is not None)
+            if ev is not None:
+                pstats.append(st)
+            return
         if ev:
             ev[0].record(stream)
         if flat:
@@ -609,11 +624,28 @@ def main():
     elapsed = time.perf_counter() - t0
     D.barrier()
     elapsed_max = D.allreduce(elapsed, "MAX")
-    search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
-    sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
+    if co:
+        # search / SW: summed launch spans of the step (overlapped with each other); the search roofline uses the
+        # average search launch, the figure rocprofv3 reports per dispatch
+        n_batches = pstats[0].n_batches
+        search_ms = float(np.mean([p.search_ms for p in pstats]))
+        sw_ms = float(np.mean([p.sw_ms for p in pstats]))
+        span_ms = float(np.mean([p.kernel_ms for p in pstats]))
+        first_search_ms = float(np.mean([p.first_search_ms for p in pstats]))
+        last_sw_ms = float(np.mean([p.last_sw_ms for p in pstats]))
+    else:
+        n_batches = 1
+        search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
+        sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
+        span_ms = search_ms + sw_ms
+        first_search_ms, last_sw_ms = search_ms, sw_ms
     if os.environ.get("DRM_BENCH_VERBOSE"):
-        print("per-step search ms", [round(e[0].elapsed_ms(e[1]), 2) for e in events],
-              "sw ms", [round(e[1].elapsed_ms(e[2]), 2) for e in events], file=sys.stderr, flush=True)
+        if co:
+            print("per-step span ms", [round(p.kernel_ms, 2) for p in pstats], "search", [round(p.search_ms, 2) for p in
+                  pstats], "sw", [round(p.sw_ms, 2) for p in pstats], file=sys.stderr, flush=True)
+        else:
+            print("per-step search ms", [round(e[0].elapsed_ms(e[1]), 2) for e in events],
+                  "sw ms", [round(e[1].elapsed_ms(e[2]), 2) for e in events], file=sys.stderr, flush=True)
 
     # correctness / quality of this rank's last step
     if flat and ix.overflows():
@@ -641,7 +673,12 @@ def main():
         bytes_q = 4 * info.d + l0 * deg0 * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
         codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
         bytes_launch = float(bytes_q.sum() + codebook)
+    # per launch: the step's search runs as n_batches launches of ~Q / n_batches queries
+    avg_launch_ms = search_ms / n_batches
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
+    # the first batch's search runs alone on the device at full occupancy
+    first_bytes = float(bytes_q[:Q // n_batches].sum()) + (0.0 if flat else float(codebook))
+    achieved_alone = first_bytes / (first_search_ms * 1e-3) / 1e9
     cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
     pkey = args.workload + ("_flat" if flat else "") + ("_gru" if args.embed == "gru" else "")
@@ -687,7 +724,11 @@ def main():
             "roofline": {"bound": "hbm", "kernel": search_kernel, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": round(search_ms, 4),
+                         "bytes_per_launch_avg": bytes_launch / n_batches, "launches_per_step": n_batches,
+                         "avg_launch_ms": round(avg_launch_ms, 4),
+                         "alone": {"frac": round(achieved_alone / HBM_PEAK_GBS, 5), "achieved": round(achieved_alone, 2),
+                                   "launch_ms": round(first_search_ms, 4),
+                                   "note": "the step's first search launch, alone on the device (full grid)"},
                          "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch, gfx950 x2 "
                                             "read correction, uncalibrated for 4-8 B random reads")
                          if traffic is not None else None,
@@ -706,7 +747,11 @@ def main():
             "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
             if enc else None,
             "l2_rerank": l2,
-            "breakdown": {"search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
+            "breakdown": {"schedule": (f"co-scheduled: {n_batches} batches, search(b) beside SW rerank(b-1) on the same "
+                                       f"CUs (drm_search_rerank_device)") if co else "sequential: search, then SW rerank",
+                          "device_span_ms": round(span_ms, 3),
+                          "search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
+                          "first_search_alone_ms": round(first_search_ms, 3), "last_sw_alone_ms": round(last_sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
                           "bytes_per_query": round(float(bytes_q.mean()), 1),

@@ -40,7 +40,7 @@ EXPORTS = [
     "drm_vectorize", "drm_vectorize_device", "drm_encoder_flags",
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
     "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
-    "drm_index_set_search_waves", "drm_refs_set_sw_waves",
+    "drm_index_set_search_waves", "drm_refs_set_sw_waves", "drm_search_rerank_device",
 ]
 
 
@@ -68,6 +68,11 @@ class FlatIndexInfo(C.Structure):
 class EncoderInfo(C.Structure):
     _fields_ = [("hidden", C.c_int32), ("emb_dim", C.c_int32), ("max_len", C.c_int32), ("out_dim", C.c_int32),
                 ("n_token_rows", C.c_int32), ("device", C.c_int32), ("h0", C.c_float), ("device_bytes", C.c_int64)]
+
+
+class PipelineStats(C.Structure):
+    _fields_ = [("nq", C.c_int64), ("n_batches", C.c_int32), ("kernel_ms", C.c_double), ("search_ms", C.c_double),
+                ("sw_ms", C.c_double), ("first_search_ms", C.c_double), ("last_sw_ms", C.c_double)]
 
 
 class SearchStats(C.Structure):
@@ -110,6 +115,8 @@ def lib():
         "drm_index_get_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
         "drm_index_set_search_waves": (C.c_int, [vp, i32]),
         "drm_refs_set_sw_waves": (C.c_int, [vp, i32]),
+        "drm_search_rerank_device": (C.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
+                                               vp, vp, vp, vp, C.POINTER(PipelineStats)]),
         "drm_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "drm_search_device_ex": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),

@@ -360,11 +360,12 @@ __global__ __launch_bounds__(64) void sw_score_kernel(RerankArgs a)
 // is not A/C/G/T but does occur in the query (e.g. N against N) cannot be coded; the query is then
 // flagged (ncand = kNeedBitProfile) and the bit-profile kernel re-scores it exactly.
 constexpr int kNeedBitProfile = -4;
-#ifndef DRM_SW_BLOCKLOAD
-#define DRM_SW_BLOCKLOAD 1 // candidate bytes by 16-byte block loads (0: one byte load per DP row)
-#endif
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+#ifndef DRM_SW_ROWS2
+#define DRM_SW_ROWS2 1 // two DP rows in flight per pass (sw_row2_f16); 0: one row at a time (sw_row_f16)
+#endif
 
 __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
 {
@@ -400,6 +401,75 @@ __device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pp, h2 &
         left = h;
         best = __builtin_elementwise_maximum(best, h);
         td = tn;
+    }
+}
+
+// Two DP rows at once, the second one column behind the first: at step j row a (candidate byte i) computes
+// column j and row b (byte i + 1) column j - 1, from the value row a has just written there. The two rows'
+// left-to-right dependency chains (max3 -> clamp -> next max3) are independent, so one wave issues from two
+// chains instead of one -- the op count per cell pair is unchanged (3.5), but a single wave per SIMD no
+// longer stalls on every cell's dependency: the rerank can then run one wave per SIMD
+// beside the search kernel.
+template <int LQ, int PF = 2>
+__device__ __forceinline__ void sw_row2_f16(h2 (&H)[LQ], const uint32_t *pa, const uint32_t *pb, h2 &best)
+{
+    const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
+    const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
+    // the profile words of both rows, 4 columns (one ds_read_b128) per group, PF groups in flight ahead of the
+    // one being consumed: a group's slot is refilled once both rows are past it. At one wave per SIMD nothing
+    // else hides the LDS latency, so the reads are issued ~8 columns (112 VALU) before their use.
+    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
+    uint4 A[NS], B[NS];
+#pragma unroll
+    for (int g = 0; g < NS; ++g)
+        if (g < NG) {
+            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
+            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
+        }
+    auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
+    h2 tda = __builtin_bit_cast(h2, A[0].x), tdb = __builtin_bit_cast(h2, B[0].x); // column 0: zero-border diagonal
+    h2 lefta = kZero, leftb = kZero;
+#pragma clang loop unroll(full)
+    for (int j = 0; j <= LQ; ++j) {
+        if ((j & 3) == 0 && j >= 4) { // group j/4 - 1 is done for both rows: refill its slot
+            const int gd = (j >> 2) - 1, gn = gd + NS;
+            if (gn < NG) {
+                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
+                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
+            }
+            __builtin_amdgcn_sched_barrier(0); // keep the reads here, ahead of the columns that consume them
+        }
+        h2 ha = kZero, hb = kZero;
+        if (j < LQ) { // row a, column j: up = the previous row's H[j]
+            const h2 up = H[j];
+            h2 tn = kZero;
+            if (j + 1 < LQ) {
+                const int n = j + 1;
+                tn = up + __builtin_bit_cast(h2, word(A[(n >> 2) % NS], n & 3));
+            }
+            h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tda, up), lefta);
+            h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
+            H[j] = h;
+            lefta = h;
+            tda = tn;
+            ha = h;
+        }
+        if (j >= 1) { // row b, column c = j - 1: up = row a's value, written at the previous step
+            const int c = j - 1;
+            const h2 up = H[c];
+            h2 tn = kZero;
+            if (c + 1 < LQ) {
+                const int n = c + 1;
+                tn = up + __builtin_bit_cast(h2, word(B[(n >> 2) % NS], n & 3));
+            }
+            h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tdb, up), leftb);
+            h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
+            H[c] = h;
+            leftb = h;
+            tdb = tn;
+            hb = h;
+        }
+        best = __builtin_elementwise_maximum(__builtin_elementwise_maximum(best, ha), hb);
     }
 }
 
@@ -482,78 +552,69 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
             // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
             // block in flight while the current one is consumed), not one byte load per row
-            if (a.genome) { // dynamic lookup: unaligned windows, one byte per row (genome bytes are ACGTN)
-                const CandRow ra(a, wa), rb(a, wb);
-                const int L = a.ref_len;
-                for (int i = 0; i < L; ++i) {
-                    const int ca = ra.at(i), cb = has_b ? rb.at(i) : -1;
-                    int ka = acgt_code(ca), kb = acgt_code(cb);
-                    if (ka < 0) { // N (or the empty window, -1): "a byte the query lacks" unless it has it
-                        flagged |= ca >= 0 && ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
-                        ka = 4;
-                    }
-                    if (kb < 0) {
-                        flagged |= cb >= 0 && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
-                        kb = 4;
-                    }
-                    sw_row_f16<LQ>(H, pprof + ka * GST + kb * PST, best);
-                }
-            } else {
-#if DRM_SW_BLOCKLOAD
+            // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
+            // block in flight while the current one is consumed), not one byte load per row; dynamic lookup reads
+            // unaligned genome windows one byte per row (genome bytes are ACGTN)
+            const CandRow ra(a, wa), rb(a, wb);
             const uint4 *pa = reinterpret_cast<const uint4 *>(a.refs + (size_t)wa * (size_t)a.row_stride);
             const uint4 *pb = reinterpret_cast<const uint4 *>(a.refs + (size_t)wb * (size_t)a.row_stride);
             const int L = a.ref_len;
             const int nblk = (int)(a.row_stride >> 4); // row_stride is a multiple of 16, >= ref_len
             uint4 ba = make_uint4(0u, 0u, 0u, 0u), bb = ba, na4 = ba, nb4 = ba;
-            if (L > 0) {
+            if (L > 0 && !a.genome) {
                 na4 = pa[0];
                 nb4 = pb[0];
             }
             uint32_t wa4 = 0u, wb4 = 0u;
-            for (int i = 0; i < L; ++i) {
-                if ((i & 15) == 0) { // wave-uniform: next block becomes current, prefetch the one after
-                    ba = na4;
-                    bb = nb4;
-                    const int nx = (i >> 4) + 1;
-                    if (nx < nblk && 16 * nx < L) {
-                        na4 = pa[nx];
-                        nb4 = pb[nx];
-                    }
-                }
-                if ((i & 3) == 0) {
-                    const int wsel = (i >> 2) & 3;
-                    wa4 = wsel == 0 ? ba.x : wsel == 1 ? ba.y : wsel == 2 ? ba.z : ba.w;
-                    wb4 = wsel == 0 ? bb.x : wsel == 1 ? bb.y : wsel == 2 ? bb.z : bb.w;
+            // profile row of DP row i (called for i = 0, 1, ... in order)
+            auto row = [&](int i) -> const uint32_t * {
+                int ca, cb;
+                if (a.genome) {
+                    ca = ra.at(i);
+                    cb = has_b ? rb.at(i) : -1;
                 } else {
-                    wa4 >>= 8;
-                    wb4 >>= 8;
+                    if ((i & 15) == 0) { // wave-uniform: next block becomes current, prefetch the one after
+                        ba = na4;
+                        bb = nb4;
+                        const int nx = (i >> 4) + 1;
+                        if (nx < nblk && 16 * nx < L) {
+                            na4 = pa[nx];
+                            nb4 = pb[nx];
+                        }
+                    }
+                    if ((i & 3) == 0) { // take the next word of the block (register moves, no indexing)
+                        wa4 = ba.x;
+                        wb4 = bb.x;
+                        ba = make_uint4(ba.y, ba.z, ba.w, 0u);
+                        bb = make_uint4(bb.y, bb.z, bb.w, 0u);
+                    } else {
+                        wa4 >>= 8;
+                        wb4 >>= 8;
+                    }
+                    ca = (int)(wa4 & 255u);
+                    cb = has_b ? (int)(wb4 & 255u) : -1;
                 }
-                const int ca = (int)(wa4 & 255u), cb = (int)(wb4 & 255u);
-#else
-            const uint8_t *pa = a.refs + (size_t)wa * (size_t)a.row_stride;
-            const uint8_t *pb = a.refs + (size_t)wb * (size_t)a.row_stride;
-            const int L = a.ref_len;
-            int na = (L > 0) ? (int)pa[0] : 0;
-            int nb2 = (L > 0) ? (int)pb[0] : 0;
-            for (int i = 0; i < L; ++i) {
-                const int ca = na, cb = nb2;
-                if (i + 1 < L) { // prefetch the next row's bytes
-                    na = pa[i + 1];
-                    nb2 = pb[i + 1];
-                }
-#endif
                 int ka = acgt_code(ca), kb = acgt_code(cb);
-                if (ka < 0) {
-                    flagged |= ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
+                if (ka < 0) { // N (or the empty window, -1): "a byte the query lacks" unless it has it
+                    flagged |= ca >= 0 && ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
                     ka = 4;
                 }
                 if (kb < 0) {
-                    flagged |= has_b && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
+                    flagged |= cb >= 0 && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
                     kb = 4;
                 }
-                sw_row_f16<LQ>(H, pprof + ka * GST + kb * PST, best);
+                return pprof + ka * GST + kb * PST;
+            };
+            int i = 0;
+#if DRM_SW_ROWS2
+            for (; i + 1 < L; i += 2) {
+                const uint32_t *p0 = row(i);
+                const uint32_t *p1 = row(i + 1);
+                sw_row2_f16<LQ>(H, p0, p1, best);
             }
-            }
+#endif
+            for (; i < L; ++i)
+                sw_row_f16<LQ>(H, row(i), best);
             const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
             a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
             a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);

@@ -6,7 +6,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._native import IndexInfo, SearchStats, check, lib, ptr
+from ._native import IndexInfo, PipelineStats, SearchStats, check, lib, ptr
 
 
 def _outputs(n, k_clusters, k, rerank):
@@ -81,6 +81,22 @@ def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None,
                                   ptr(o.get("status")), C.byref(st)))
     o["stats"] = st
     return o
+
+
+def search_rerank_device(index, table, d_x, n, d_queries, d_q_len, q_stride, d_D, d_I, d_sw_scores, d_sw_ids,
+                         d_status, k=128, ef=128, k_clusters=None, stride=1, d_ndis=None, d_nhops=None,
+                         d_nhops_upper=None, stream=None, stats=False):
+    """drm_search_rerank_device: search + SW rerank on DeviceBuffers, the search of batch b beside the rerank
+    of batch b-1 on the same CUs. stats=True synchronises and returns the PipelineStats."""
+    kc = k if k_clusters is None else k_clusters
+    st = PipelineStats() if stats else None
+    p = lambda b: b.ptr if b is not None else None  # noqa: E731
+    check(lib().drm_search_rerank_device(index.handle, table.handle, d_x.ptr, int(n), int(kc), int(ef), d_queries.ptr,
+                                         d_q_len.ptr, int(q_stride), int(stride), int(k), d_D.ptr, d_I.ptr, p(d_ndis),
+                                         p(d_nhops), p(d_nhops_upper), d_sw_scores.ptr, d_sw_ids.ptr, d_status.ptr,
+                                         stream.handle if stream is not None else None,
+                                         C.byref(st) if st is not None else None))
+    return st
 
 
 class MultiIndex:

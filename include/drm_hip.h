@@ -271,6 +271,30 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
                       int32_t k, float *D, int64_t *I, int32_t *sw_scores, uint64_t *sw_ids, int32_t *status,
                       drm_search_stats *stats);
 
+/* The same search -> SW rerank on DEVICE-resident buffers (shapes as drm_search_rerank; d_ndis, d_nhops,
+ * d_nhops_upper may be NULL), enqueued behind the caller's work on `stream` and joined back into it. The n
+ * queries run as DRM_CO_BATCHES batches (default 1) on two internal streams, search(b) beside rerank(b-1) on the
+ * same CUs with capped grids (DRM_CO_SEARCH_WAVES = 8 search and DRM_CO_SW_WAVES = 4 rerank waves per CU), so the
+ * rerank's VALU work can fill issue slots the memory-bound search leaves idle (measured: no faster at C5 on
+ * MI355X, DESIGN.md sec. 5 -- hence one batch by default: the search, then the rerank, each with the whole chip).
+ * The outputs equal those of drm_search_device + drm_post_process_sw_static_device (or _dynamic_device for a
+ * genome handle) over the whole batch. d_status must be checked by the caller. stats (may be NULL) makes the call
+ * synchronous and returns the device span and the summed search / rerank launch spans. */
+typedef struct {
+    int64_t nq;
+    int32_t n_batches;
+    double kernel_ms;       /* device span: first search start -> last rerank end */
+    double search_ms;       /* sum of the search launches' spans (overlapped ones included) */
+    double sw_ms;           /* sum of the rerank launches' spans */
+    double first_search_ms; /* the first search, alone on the device */
+    double last_sw_ms;      /* the last rerank, alone on the device */
+} drm_pipeline_stats;
+int drm_search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, int64_t n, int32_t k_clusters,
+                             int32_t ef, const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
+                             int64_t stride, int32_t k, float *d_D, int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops,
+                             int32_t *d_nhops_upper, int32_t *d_sw_scores, uint64_t *d_sw_ids, int32_t *d_status,
+                             void *stream, drm_pipeline_stats *stats);
+
 /* Optional: set up drm_search_rerank's streams and device buffers for a batch of n queries ahead of the
  * call (q_stride = 0: search only), and do the first-use work there (the copy engines' first DMA, the
  * search kernel's first launch), so the call itself only streams data and runs kernels. */

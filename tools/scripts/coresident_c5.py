@@ -25,6 +25,7 @@ ap.add_argument("--embed", default="gru")
 ap.add_argument("--chunks", default="4,6,8")
 ap.add_argument("--search-waves", default="12,11")
 ap.add_argument("--sw-waves", default="4")
+ap.add_argument("--lockstep", action="store_true", help="also time the script-level lockstep schedule")
 a = ap.parse_args()
 args = argparse.Namespace(cache="/tmp/drm_bench_cache", queries=a.queries, embed=a.embed)
 D = bench.Dist()
@@ -41,10 +42,14 @@ s0, s1 = Stream(), Stream()
 L = lib()
 
 
+d_nd0, d_nh0 = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
+
+
 def search(lo, hi, st, waves):
+    # ndis / nhops buffers given: without them drm_search_device_ex allocates a temporary and synchronises
     check(L.drm_index_set_search_waves(ix.handle, waves))
     check(L.drm_search_device_ex(ix.handle, d_x.ptr + lo * 512, hi - lo, K, 128, d_D.ptr + lo * K * 4,
-                                 d_I.ptr + lo * K * 8, None, None, None, st.handle))
+                                 d_I.ptr + lo * K * 8, d_nd0.ptr + lo * 4, d_nh0.ptr + lo * 4, None, st.handle))
 
 
 def sw(lo, hi, st, waves):
@@ -113,7 +118,15 @@ for w in (0,) + tuple(int(x) for x in a.sw_waves.split(",")):
 ms = timed(seq)
 ref_id, ref_sc = d_id.download(), d_sc.download()
 print(f"sequential (search 20 + SW uncapped): {ms:.1f} ms  {Q / ms * 1e3 / 1e6:.3f} M reads/s", flush=True)
-for P in (int(x) for x in a.chunks.split(",")):
+# independent pair: the search of all reads on s0 beside the SW of all reads (the previous run's neighbours) on s1
+for ws in (int(x) for x in a.search_waves.split(",")):
+    for wsw in (int(x) for x in a.sw_waves.split(",")):
+        def pair():
+            search(0, Q, s0, ws)
+            sw(0, Q, s1, wsw)
+        ms = timed(pair)
+        print(f"independent pair: search {ws} waves/CU on s0 beside SW {wsw} waves/CU on s1: {ms:.1f} ms", flush=True)
+for P in (int(x) for x in a.chunks.split(",")) if a.lockstep else ():
     for ws in (int(x) for x in a.search_waves.split(",")):
         for wsw in (int(x) for x in a.sw_waves.split(",")):
             d_id.zero()
@@ -123,3 +136,22 @@ for P in (int(x) for x in a.chunks.split(",")):
                   f"  identical={same}", flush=True)
 check(L.drm_index_set_search_waves(ix.handle, 0))
 check(L.drm_refs_set_sw_waves(table.handle, 0))
+
+# the library's own co-scheduled entry point (drm_search_rerank_device)
+import os  # noqa: E402
+from deepreadmapper_amd.executor import search_rerank_device  # noqa: E402
+d_nd, d_nh, d_nu = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
+for P in (int(x) for x in a.chunks.split(",")):
+    for ws in (int(x) for x in a.search_waves.split(",")):
+        os.environ.update(DRM_CO_BATCHES=str(P), DRM_CO_SEARCH_WAVES=str(ws), DRM_CO_SW_WAVES=a.sw_waves.split(",")[-1])
+        d_id.zero()
+        best = None
+        for _ in range(3):
+            st = search_rerank_device(ix, table, d_x, Q, d_q, d_ql, q.shape[1], d_D, d_I, d_sc, d_id, d_st, k=K,
+                                      ef=128, d_ndis=d_nd, d_nhops=d_nh, d_nhops_upper=d_nu, stream=s0, stats=True)
+            best = st if best is None or st.kernel_ms < best.kernel_ms else best
+        same = np.array_equal(d_id.download(), ref_id) and np.array_equal(d_sc.download(), ref_sc)
+        print(f"drm_search_rerank_device P={P} search {ws}: span {best.kernel_ms:.1f} ms "
+              f"({Q / best.kernel_ms * 1e3 / 1e6:.3f} M reads/s), search launches {best.search_ms:.1f}, SW launches "
+              f"{best.sw_ms:.1f}, first search {best.first_search_ms:.1f}, last SW {best.last_sw_ms:.1f}  "
+              f"identical={same}", flush=True)

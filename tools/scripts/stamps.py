@@ -13,11 +13,13 @@ from deepreadmapper_amd.device import DeviceBuffer, synchronize  # noqa: E402
 from deepreadmapper_amd.search import HnswPqIndex  # noqa: E402
 from deepreadmapper_amd._native import lib, check  # noqa: E402
 
-if len(sys.argv) > 1 and sys.argv[1] == "c5":  # bench.py --workload c5 must have run (its cache files)
-    g = synth.genome(25_000_149, seed=44)
-    reads, _ = synth.simulate_reads_range(g, 0, 1_250_000, seed=9)
-    q_emb = synth.embed(synth.tag(reads))
-    index_path = "/tmp/drm_bench_cache/c5_M16_efc200_s1_gpu.index"
+if len(sys.argv) > 1 and sys.argv[1] in ("c5", "c5gru"):  # the bench's C5 workload (built here if absent)
+    import argparse
+    import bench
+    args = argparse.Namespace(cache="/tmp/drm_bench_cache", queries=1_250_000,
+                              embed="gru" if sys.argv[1] == "c5gru" else "kmer3")
+    wl = bench.prepare_c5(args, bench.Dist(), 0)
+    q_emb, index_path = wl["q_emb"], wl["index_path"]
 else:
     w = synth.Workload("c3", 500_149, 100_000, seed=42, read_seed=7).generate("/tmp/drm_bench_cache")
     q_emb, index_path = w.q_emb, w.index_path
