@@ -530,9 +530,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             clear_n += nf;
             DRM_FSTAMP(4);
             // add_to_heap for each fresh link in row order. On a full heap the root distance only
-            // falls, so a link at or above it now is rejected for the whole row: it is skipped here.
+            // falls, so a link at or above it now is rejected for the whole row: it is skipped here. It cannot
+            // enter a k < ef result set either: the heap keeps the ef smallest pushed keys (popped slots keep
+            // theirs), so its root is at or above the k-th smallest result, the threshold add_result tests.
             uint64_t rem = fm, accm = 0;
-            if (LOGRES && kc == ef)
+            if (kc == ef)
                 rem &= ballot(dk < hi32(root));
             while (rem) {
                 const int l = __builtin_ctzll(rem);

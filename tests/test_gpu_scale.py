@@ -45,7 +45,7 @@ def c4():
     w = synth.Workload("c4", 20_000_299, 1_000_000, stride=4, seed=43, read_seed=8).generate(
         CACHE, need_refs=False, gpu_build=True)
     fx = faiss_file.read(w.index_path)
-    assert fx.ntotal == 10_000_000
+    assert fx.ntotal == 2 * ((20_000_299 - 150) // 4 + 1)  # 10,000,076 fwd/RC windows at stride 4
     return {"w": w, "fx": fx}
 
 

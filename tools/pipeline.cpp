@@ -288,13 +288,14 @@ int main(int argc, char *argv[])
                       << std::endl;
         // one pass over queries [lo, lo + m) into the output arrays at row lo
         auto run = [&](size_t lo, size_t m, drm_search_stats *sp) {
-            const uint8_t *qb = is_npy ? nullptr : qbuf.p + lo * qs;
+            const bool search_only = sam_from_search || sam_l2 || sam_header_only;
+            const uint8_t *qb = (is_npy || search_only) ? nullptr : qbuf.p + lo * qs;
             if (multi)
                 return drm_multi_search_rerank(multi, x.p + lo * dim, (int64_t)m, (int32_t)dim, k_clusters, ef, qb,
                                                ql.p + lo, (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters,
                                                I.p + lo * k_clusters, sw_scores.p + lo * k, sw_ids.p + lo * k,
                                                status.p + lo, sp);
-            return drm_search_rerank(index, (sam_from_search || sam_l2) ? nullptr : rt, x.p + lo * dim, (int64_t)m,
+            return drm_search_rerank(index, search_only ? nullptr : rt, x.p + lo * dim, (int64_t)m,
                                      (int32_t)dim,
                                      k_clusters, ef, qb, ql.p + lo,
                                      (int32_t)qs, (int64_t)stride, k, D.p + lo * k_clusters, I.p + lo * k_clusters,
