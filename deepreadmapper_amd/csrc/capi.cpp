@@ -82,8 +82,8 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 
 void free_index(drm::DeviceIndex &d)
 {
-    void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr,
-                    d.visited,   d.clear_list, d.counter, d.stamps,   d.fb_list, d.log};
+    void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
+                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -253,6 +253,8 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.log_cap_req = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("DRM_SEARCH_FAST"))
             d.use_fast = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_INLINE"))
+            d.use_inline = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
             d.try_sorted = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
@@ -268,6 +270,8 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.nbr0 = upload_vec(nbr0, d.device_bytes);
             d.upper_off = upload_vec(upper_off, d.device_bytes);
             d.upper_nbr = upload_vec(upper, d.device_bytes);
+            if (d.use_inline)
+                drm::build_inline_rows(d); // ids + inline codes per level-0 row (lean kernel)
             drm::reserve_search_scratch(d); // the per-slot search workspace, once, outside any search
         } catch (...) {
             free_index(d);

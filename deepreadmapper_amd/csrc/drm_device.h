@@ -60,6 +60,12 @@ struct DeviceIndex {
     float *centroids = nullptr;    // [M][ksub][dsub] f32
     uint8_t *codes = nullptr;      // [ntotal][code_size]
     int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
+    // lean kernel's level-0 rows with the neighbours' PQ codes inline: node i's row is deg0 ids (int32) then
+    // deg0 8-byte codes, row_words int32 per row (384 B at M_hnsw = 16), so one row fetch brings the codes the
+    // hop's distances need; null when the index shape has no such layout (PQ != 8 x 8)
+    int32_t *rows = nullptr;
+    int32_t row_words = 0;
+    int32_t use_inline = 1;        // DRM_SEARCH_INLINE=0: the lean kernel reads nbr0 + codes instead
     uint32_t *upper_off = nullptr; // [ntotal] start of node's level>=1 lists in upper_nbr, ~0u if none
     int32_t *upper_nbr = nullptr;  // concatenated level>=1 lists
     int64_t upper_len = 0;
@@ -113,11 +119,15 @@ struct SearchArgs {
     uint32_t *fb_count;
     uint64_t *log;         // lean kernel: per-slot log of accepted MinimaxHeap pushes
     int32_t log_cap;
+    const int32_t *rows;   // lean kernel, inline layout: [ntotal][row_words] ids + codes (DeviceIndex::rows)
+    int32_t row_words;
 };
 
 // lean kernel (hnsw_pq_fast.hip): PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc);
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream);
+// DeviceIndex::rows from nbr0 + codes (PQ 8 x 8, deg0 <= 64), on the device
+void build_inline_rows(DeviceIndex &ix);
 
 void reserve_search_scratch(DeviceIndex &ix);
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,

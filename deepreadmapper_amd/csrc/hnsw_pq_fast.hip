@@ -20,6 +20,7 @@
 //     selects + sorts the k results once per query. k < ef keeps a register result set (k <= 64).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "drm_device.h"
@@ -335,7 +336,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
 // the pipeline's EF = K = 128 on a clean index, and the sparse default k_clusters = 5 at EF = 128
 // (src/main.cpp:56-63,278) -- fewer live SGPRs (no spills to VGPR lanes, no kernel-argument reloads
 // inside the hop loop) and no duplicate-link pass.
-template <bool LOGRES, bool STAMPS, bool FIX128>
+// INL: the level-0 rows carry their neighbours' PQ codes (SearchArgs::rows): one row fetch gives a hop its
+// distances, the next row is predicted and prefetched from them while the visited-bitmap test is in flight,
+// and only that test's round trip stays on the hop's critical path.
+template <bool LOGRES, bool STAMPS, bool FIX128, bool INL = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -426,6 +430,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         bool spec = false;
         uint2 c8_pref = make_uint2(0u, 0u);
         uint32_t vw_pref = 0u;
+        // INL: a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row
+        // prediction can skip links back to nodes already expanded before the visited test has answered
+        uint32_t popped_bits = 0u;
+        auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
         while (nvalid > 0) {
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
@@ -462,7 +470,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // expand v0's level-0 row (one coalesced load, lane j = link j)
             int32_t v1 = v1_pref;
             const bool hit = v0 == pred;
-            if (!hit)
+            if (INL) {
+                const uint32_t h0 = pop_hash(v0);
+                if (lane == (int)((h0 >> 5) & 63u))
+                    popped_bits |= 1u << (h0 & 31u);
+                if (!hit) {
+                    const int32_t *row = a.rows + (size_t)v0 * (size_t)a.row_words;
+                    v1 = lane < deg0 ? row[lane] : -1;
+                    c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(row + deg0)[lane] : make_uint2(0u, 0u);
+                }
+            } else if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
             const uint64_t negm = ballot(v1 < 0) & deg0m;
             const int jmax = negm ? __builtin_ctzll(negm) : deg0;
@@ -471,13 +488,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             uint2 c8 = make_uint2(0u, 0u);
             uint32_t old = 0xFFFFFFFFu;
             const uint32_t bit = 1u << (v1 & 31);
-            const bool use_spec = DRM_PQ_SPEC && hit && spec;
-            if (use_spec) {
+            const bool use_spec = !INL && DRM_PQ_SPEC && hit && spec;
+            if (INL) {
+                c8 = c8_pref; // arrived with the row
+                if (act)
+                    old = vis_test_set(&vis[v1 >> 5], bit); // in flight while the distances are formed
+            } else if (use_spec) {
                 c8 = c8_pref;
                 old = act ? vw_pref : 0xFFFFFFFFu;
             } else if (act) {
                 c8 = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1 * 8); // overlaps the visited test
                 old = vis_test_set(&vis[v1 >> 5], bit);
+            }
+            uint32_t dall = 0xFFFFFFFFu;
+            if (INL) {
+                // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min:
+                // the smallest valid heap slot or active link not known to be popped; its row (ids + codes) is
+                // fetched now, beside the visited test
+                float lv[8];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    lv[m] = lut[m * 256 + ((c8.x >> (8 * m)) & 255u)];
+                    lv[m + 4] = lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                float r = 0.0f;
+#pragma unroll
+                for (int m = 0; m < 8; ++m)
+                    r = __fadd_rn(r, lv[m]);
+                dall = ord32(r);
+                const uint32_t hv = pop_hash(v1);
+                const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
+                const bool known_popped = (pw >> (hv & 31u)) & 1u;
+                const uint32_t dp = (act && !known_popped) ? dall : 0xFFFFFFFFu;
+                const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
+                const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
+                uint32_t mk = dp < hL ? dp : hL;
+                mk = mk < hR ? mk : hR;
+                const int32_t mid = dp == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
+                const uint32_t mm = wave_min_u32(mk);
+                pred = -1;
+                if (mm != 0xFFFFFFFFu) {
+                    pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
+                    const int32_t *prow = a.rows + (size_t)pred * (size_t)a.row_words;
+                    v1_pref = lane < deg0 ? prow[lane] : -1;
+                    c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(prow + deg0)[lane] : make_uint2(0u, 0u);
+                }
             }
             bool fresh = act && (old & bit) == 0u;
             if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
@@ -496,6 +552,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
             // on the fresh ones)
             // all 8 LDS reads in flight before the first add (the adds stay in sub-quantizer order)
+            uint32_t dk;
+            if (INL) {
+                dk = fresh ? dall : 0xFFFFFFFFu;
+            } else {
             float lv[8];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -507,8 +567,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 #pragma unroll
             for (int m = 0; m < 8; ++m)
                 r = __fadd_rn(r, lv[m]);
-            const uint32_t dk = fresh ? ord32(r) : 0xFFFFFFFFu;
-            {
+            dk = fresh ? ord32(r) : 0xFFFFFFFFu;
+            }
+            if (!INL) {
                 // prefetch the row of the likely next pop_min (smallest valid slot or fresh link)
                 const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
                 const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
@@ -583,7 +644,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             nstep++;
             spec = false;
-            if (DRM_PQ_SPEC && pred >= 0) {
+            if (!INL && DRM_PQ_SPEC && pred >= 0) {
                 const uint64_t pneg = ballot(lane < deg0 && v1_pref < 0);
                 const int pmax = pneg ? __builtin_ctzll(pneg) : deg0;
                 if (lane < pmax) {
@@ -649,7 +710,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
+// DeviceIndex::rows: row i = nbr0[i][0 .. deg0) then, for each link, its 8-byte code (0 past the row's end).
+// One wave per node; lane j < deg0 writes link j's id and code.
+__global__ __launch_bounds__(256) void build_inline_rows_kernel(const int32_t *nbr0, const uint8_t *codes, int64_t n,
+                                                                int deg0, int row_words, int32_t *rows)
+{
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int j = threadIdx.x & 63;
+    if (i >= n || j >= deg0)
+        return;
+    const int32_t v = nbr0[i * deg0 + j];
+    int32_t *row = rows + i * (int64_t)row_words;
+    row[j] = v;
+    reinterpret_cast<uint2 *>(row + deg0)[j] = v >= 0 ? *reinterpret_cast<const uint2 *>(codes + (size_t)v * 8)
+                                                      : make_uint2(0u, 0u);
+}
+
 } // namespace
+
+void build_inline_rows(DeviceIndex &ix)
+{
+    if (ix.pq_M != 8 || ix.pq_nbits != 8 || ix.code_size != 8 || ix.deg0 > 64 || ix.deg0 < 1 || ix.vmode != 0 ||
+        ix.ntotal <= 0)
+        return;
+    const int64_t words = ((int64_t)ix.deg0 * 3 + 31) / 32 * 32; // deg0 ids + 2 deg0 code words, 128-B rows
+    DRM_HIP_CHECK(malloc_big((void **)&ix.rows, sizeof(int32_t) * (size_t)ix.ntotal * (size_t)words, kBigIndex));
+    ix.row_words = (int32_t)words;
+    ix.device_bytes += (int64_t)sizeof(int32_t) * ix.ntotal * words;
+    const int64_t blocks = (ix.ntotal + 3) / 4;
+    for (int64_t b0 = 0; b0 < blocks; b0 += (int64_t)1 << 30) {
+        const int64_t nb = std::min<int64_t>(blocks - b0, (int64_t)1 << 30);
+        hipLaunchKernelGGL(build_inline_rows_kernel, dim3((unsigned)nb), dim3(256), 0, 0, ix.nbr0 + b0 * 4 * ix.deg0,
+                           ix.codes, std::min<int64_t>(ix.ntotal - b0 * 4, nb * 4), ix.deg0, (int)words,
+                           ix.rows + b0 * 4 * words);
+        DRM_HIP_CHECK(hipGetLastError());
+    }
+    DRM_HIP_CHECK(hipDeviceSynchronize());
+}
 
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 {
@@ -661,7 +758,18 @@ void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps
 {
     const bool logres = a.k == a.ef;
     const bool fix = a.ef == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
-    if (fix && logres)
+    const bool inl = a.rows != nullptr;
+    if (fix && logres && inl)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (fix && inl)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (inl && logres && stamps)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (inl && logres)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (inl)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false, true>), dim3(slots), dim3(64), lds, stream, a);
+    else if (fix && logres)
         hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), lds, stream, a);
     else if (fix)
         hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true>), dim3(slots), dim3(64), lds, stream, a);
