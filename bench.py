@@ -34,10 +34,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
-SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8) launch (hnsw_pq_fast.hip)
+SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, true>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline codes) launch (hnsw_pq_fast.hip)
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<152>"
-SW_VALU_PER_CELL = 556 / 152 / 2  # static ISA count of the sw_score_f16_kernel<152> row loop: 556 VALU per 152 cell pairs
+SW_VALU_PER_CELL_PAIR = 1067 / 304  # static ISA count of sw_score_f16_kernel<152>'s two-row block: 1067 VALU per 2 x 152 cell pairs
+SW_PACKED_ISSUE_CYC = 4.0  # cycles per wave64 packed-f16 VALU instruction per SIMD (profiles/r02/valu_rate_probe.txt)
 
 
 def cpu_model():
@@ -262,13 +263,15 @@ def encoder_timing(d_q, Q, q_stride, dev, reps=3):
         st.synchronize()
         ts.append(a.elapsed_ms(b))
     ms = float(np.mean(ts))
-    flop_read = 2 * 123 * 3 * 64 * 2 * ((64 + 64 + 64) + (128 + 256))
+    flop_read = 2 * 123 * 3 * 64 * 2 * ((64 + 64 + 64) + (128 + 256))  # issued: the f32 state as hi + lo f16 terms
+    useful_read = 2 * 123 * 3 * 64 * 2 * ((64 + 64) + (64 + 128))      # the model's own products (h and x once)
     tflops = Q * flop_read / (ms * 1e-3) / 1e12
     und, short = enc.flags()
     enc.free()
     return {"kernel": "gru_encode_kernel", "ms": round(ms, 3), "reads_per_s": round(Q / (ms * 1e-3), 1),
             "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": ENC_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / ENC_PEAK_TFLOPS, 4)},
+                         "frac": round(tflops / ENC_PEAK_TFLOPS, 4), "counts": "issued MFMA flops (hi/lo split of the f32 state)",
+                         "useful_frac": round(tflops * useful_read / flop_read / ENC_PEAK_TFLOPS, 4)},
             "flop_per_read": flop_read, "undefined_tokens": und + short,
             "note": "Vectorizer::vectorize on the GPU; not inside `value` (the north star's path starts at embeddings)"}
 
@@ -689,8 +692,16 @@ def main():
     sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, pkey)
     ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
     sw_gcups = cells / (sw_ms * 1e-3) / 1e9
-    # VALU issue ceiling of the SW DP: 4 SIMD x 16 lanes per CU, 2 cells per packed lane-op
-    sw_peak_gcups = ncu * 64 * CLOCK_HZ / SW_VALU_PER_CELL / 1e9
+    # SW roofline = the hardware's VALU issue rate: 4 SIMDs per CU, one packed-f16 wave64 instruction per SIMD every
+    # SW_PACKED_ISSUE_CYC cycles. Instructions per launch: the committed PMC count of this workload's SW kernel when
+    # there is one (SQ_INSTS_VALU per dispatch, scaled to this run's cells), else the static DP count (one wave
+    # instruction advances 64 lanes x 2 candidates by one cell; 3.51 per cell pair)
+    sw_peak_instr = ncu * 4 * CLOCK_HZ / SW_PACKED_ISSUE_CYC
+    sw_instr_static = cells / 128.0 * SW_VALU_PER_CELL_PAIR
+    sw_instr, sw_instr_src = sw_instr_static, "static ISA count of the DP block"
+    if sw_pmc and "SQ_INSTS_VALU" in sw_pmc and (Q, K) == (1_250_000, 128):
+        sw_instr, sw_instr_src = float(sw_pmc["SQ_INSTS_VALU"]), f"{sw_prof_path}: SQ_INSTS_VALU per dispatch"
+    sw_achieved_instr = sw_instr / (sw_ms * 1e-3)
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
@@ -735,12 +746,13 @@ def main():
                          "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
                          if pmc and "valu_issue_frac" in pmc else None,
                          "issue": issue_ceiling(pmc, float(nhops.sum()), search_ms)},
-            "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_gcups, 1),
-                            "peak": round(sw_peak_gcups, 1), "unit": "GCUPS",
-                            "frac": round(sw_gcups / sw_peak_gcups, 4),
-                            "valu_ops_per_cell": SW_VALU_PER_CELL,
-                            "valu_issue_frac_pmc": round(sw_pmc["valu_issue_frac"], 3)
-                            if sw_pmc and "valu_issue_frac" in sw_pmc else None},
+            "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_achieved_instr / 1e9, 2),
+                            "peak": round(sw_peak_instr / 1e9, 2), "unit": "G wave-instr/s (packed f16 VALU issue)",
+                            "frac": round(sw_achieved_instr / sw_peak_instr, 4), "instr_per_launch": sw_instr,
+                            "instr_source": sw_instr_src, "gcups": round(sw_gcups, 1),
+                            "valu_per_cell_pair": round(SW_VALU_PER_CELL_PAIR, 3),
+                            "note": "frac = VALU issue slots used / the SIMDs' packed-issue capacity (4 SIMDs x 2.4 GHz / "
+                                    "4 cycles per CU); the DP's op count per cell pair is reported separately"},
             "cpu_baseline": cpu,
             "gather": gather,
             "host_path": host,

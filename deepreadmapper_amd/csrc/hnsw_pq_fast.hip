@@ -470,6 +470,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // expand v0's level-0 row (one coalesced load, lane j = link j)
             int32_t v1 = v1_pref;
             const bool hit = v0 == pred;
+            if (STAMPS) { // row prediction hits / hops
+                st_acc[8] += hit ? 1u : 0u;
+                st_acc[9] += 1u;
+            }
             if (INL) {
                 const uint32_t h0 = pop_hash(v0);
                 if (lane == (int)((h0 >> 5) & 63u))
