@@ -83,7 +83,7 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 void free_index(drm::DeviceIndex &d)
 {
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
-                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows};
+                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);

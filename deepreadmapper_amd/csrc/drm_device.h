@@ -65,6 +65,7 @@ struct DeviceIndex {
     // hop's distances need; null when the index shape has no such layout (PQ != 8 x 8)
     int32_t *rows = nullptr;
     int32_t row_words = 0;
+    uint2 *upper_codes = nullptr;  // the code of every upper_nbr entry (0 for -1): greedy hops fetch ids + codes together
     int32_t use_inline = 1;        // DRM_SEARCH_INLINE=0: the lean kernel reads nbr0 + codes instead
     uint32_t *upper_off = nullptr; // [ntotal] start of node's level>=1 lists in upper_nbr, ~0u if none
     int32_t *upper_nbr = nullptr;  // concatenated level>=1 lists
@@ -121,6 +122,7 @@ struct SearchArgs {
     int32_t log_cap;
     const int32_t *rows;   // lean kernel, inline layout: [ntotal][row_words] ids + codes (DeviceIndex::rows)
     int32_t row_words;
+    const uint2 *upper_codes; // lean kernel, inline layout: codes beside upper_nbr (DeviceIndex::upper_codes)
 };
 
 // lean kernel (hnsw_pq_fast.hip): PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64

@@ -259,6 +259,53 @@ __device__ __forceinline__ void sort128(uint64_t &x0, uint64_t &x1, int lane)
     }
 }
 
+// greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss], the inline
+// layout's form of greedy_upper (pq_common.h): a hop loads its upper-level list and the links' codes together
+// (SearchArgs::upper_codes), one memory round trip per hop instead of two. Same distances, same order.
+__device__ __forceinline__ void greedy_upper_inl(const SearchArgs &a, const float *lut, int lane, int32_t &nearest_out,
+                                                 uint32_t &dn_out, int &ndis_out, int &nhops_out)
+{
+    int32_t nearest = a.entry_point;
+    uint32_t dn = ufirst(ord32(pq_distance_code<true>(a, lut, nearest, load_code8<true>(a, nearest))));
+    int ndis = 0, nhops = 0;
+    for (int level = a.max_level; level >= 1; --level) {
+        const int cnt = a.cum[level + 1] - a.cum[level];
+        for (;;) {
+            const int32_t prev = nearest;
+            const uint32_t base = a.upper_off[nearest] + (uint32_t)(a.cum[level] - a.cum[1]);
+            int32_t v = -1;
+            uint2 c8 = make_uint2(0u, 0u);
+            if (lane < cnt) {
+                v = a.upper_nbr[base + lane];
+                c8 = a.upper_codes[base + lane];
+            }
+            const uint64_t neg = __ballot(lane < cnt && v < 0);
+            const int nvalid = neg ? (__ffsll((unsigned long long)neg) - 1) : cnt;
+            uint32_t dk = 0xFFFFFFFFu;
+            if (lane < nvalid)
+                dk = ord32(pq_distance_code<true>(a, lut, v, c8));
+            ndis += nvalid;
+            nhops += 1;
+            // sequential `if (dis < d_nearest)` in link order == first lane holding the minimum
+            uint64_t key = (lane < nvalid) ? (((uint64_t)dk << 32) | (uint32_t)lane) : ~0ull;
+            key = wave_min_u64(key);
+            if (key != ~0ull) {
+                const uint32_t bk = (uint32_t)(key >> 32);
+                if (bk < dn) {
+                    dn = bk;
+                    nearest = __builtin_amdgcn_readlane(v, (int)(key & 63));
+                }
+            }
+            if (nearest == prev)
+                break;
+        }
+    }
+    nearest_out = nearest;
+    dn_out = dn;
+    ndis_out = ndis;
+    nhops_out = nhops;
+}
+
 __device__ __forceinline__ uint64_t log_load(const uint64_t *lg, int i)
 {
     return __hip_atomic_load(lg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -315,6 +362,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     }
     return cnt;
 }
+
+#ifndef DRM_PQ_VIS_LOAD
+#define DRM_PQ_VIS_LOAD 1 // inline kernel: visited test by an L2 load, fresh links marked afterwards (0: test-and-set)
+#endif
 
 #ifndef DRM_PQ_SPEC
 #define DRM_PQ_SPEC 0 // codes + visited words of the predicted next row loaded one hop ahead (measured slower)
@@ -387,7 +438,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         int32_t nearest;
         uint32_t dn;
         int ndis, nhops;
-        greedy_upper<true>(a, lut, lane, nearest, dn, ndis, nhops);
+        if (INL && a.upper_codes)
+            greedy_upper_inl(a, lut, lane, nearest, dn, ndis, nhops);
+        else
+            greedy_upper<true>(a, lut, lane, nearest, dn, ndis, nhops);
         const int nhops_upper = nhops;
         DRM_FSTAMP(1);
 
@@ -495,8 +549,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const bool use_spec = !INL && DRM_PQ_SPEC && hit && spec;
             if (INL) {
                 c8 = c8_pref; // arrived with the row
+                // the visited test is in flight while the distances are formed. DRM_PQ_VIS_LOAD: a plain L2 load
+                // (sc1: this wave's own earlier marks are at L2, never in its L1), and only the fresh links are
+                // marked afterwards -- a test-and-set on every link dirtied a bitmap sector per link, visited or
+                // not. Exact: this wave alone writes its bitmap, its earlier marks were issued before this load,
+                // and a repeated id in one row is fresh once (check_dups below) and so marked once.
                 if (act)
-                    old = vis_test_set(&vis[v1 >> 5], bit); // in flight while the distances are formed
+                    old = DRM_PQ_VIS_LOAD ? __hip_atomic_load(&vis[v1 >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : vis_test_set(&vis[v1 >> 5], bit);
             } else if (use_spec) {
                 c8 = c8_pref;
                 old = act ? vw_pref : 0xFFFFFFFFu;
@@ -547,8 +607,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         fresh = false;
                 }
             }
-            if (use_spec && fresh) // the test was a load: mark the fresh links (non-returning atomics)
-                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((use_spec || (INL && DRM_PQ_VIS_LOAD)) && fresh) // the test was a load: mark the
+                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); // fresh links
             DRM_FSTAMP(3);
             const uint64_t fm = check_dups ? ballot(fresh) : ballot((old & bit) == 0u) & actm;
             const int nf = __builtin_popcountll(fm);
@@ -730,6 +790,16 @@ __global__ __launch_bounds__(256) void build_inline_rows_kernel(const int32_t *n
                                                       : make_uint2(0u, 0u);
 }
 
+__global__ __launch_bounds__(256) void build_upper_codes_kernel(const int32_t *upper_nbr, const uint8_t *codes, int64_t n,
+                                                                uint2 *out)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t v = upper_nbr[i];
+    out[i] = v >= 0 ? *reinterpret_cast<const uint2 *>(codes + (size_t)v * 8) : make_uint2(0u, 0u);
+}
+
 } // namespace
 
 void build_inline_rows(DeviceIndex &ix)
@@ -748,6 +818,17 @@ void build_inline_rows(DeviceIndex &ix)
                            ix.codes, std::min<int64_t>(ix.ntotal - b0 * 4, nb * 4), ix.deg0, (int)words,
                            ix.rows + b0 * 4 * words);
         DRM_HIP_CHECK(hipGetLastError());
+    }
+    if (ix.upper_len > 0) {
+        DRM_HIP_CHECK(malloc_big((void **)&ix.upper_codes, sizeof(uint2) * (size_t)ix.upper_len, kBigIndex));
+        ix.device_bytes += (int64_t)sizeof(uint2) * ix.upper_len;
+        const int64_t ub = (ix.upper_len + 255) / 256;
+        for (int64_t b0 = 0; b0 < ub; b0 += (int64_t)1 << 30) {
+            const int64_t nb = std::min<int64_t>(ub - b0, (int64_t)1 << 30);
+            hipLaunchKernelGGL(build_upper_codes_kernel, dim3((unsigned)nb), dim3(256), 0, 0, ix.upper_nbr + b0 * 256,
+                               ix.codes, std::min<int64_t>(ix.upper_len - b0 * 256, nb * 256), ix.upper_codes + b0 * 256);
+            DRM_HIP_CHECK(hipGetLastError());
+        }
     }
     DRM_HIP_CHECK(hipDeviceSynchronize());
 }

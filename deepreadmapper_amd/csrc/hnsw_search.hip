@@ -1145,6 +1145,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
         a.log_cap = ix.log_cap;
         a.rows = ix.rows;
         a.row_words = ix.row_words;
+        a.upper_codes = ix.upper_codes;
         DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 3 * sizeof(uint32_t), stream));
         launch_hnsw_pq_fast(a, slots, lds, ix.stamps != nullptr, stream);
         return;
