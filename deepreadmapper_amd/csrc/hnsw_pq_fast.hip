@@ -64,6 +64,12 @@ __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // la
     return ((uint64_t)h << 32) | o;
 }
 
+#ifndef DRM_PQ_AHEAD
+// INL: the visited test of the predicted next row is issued before this hop's push loop, and the row after
+// that is predicted and fetched then too (two hops ahead), so the test's round trip overlaps the push loop
+#define DRM_PQ_AHEAD 0
+#endif
+
 #ifndef DRM_PQ_VPATH
 #define DRM_PQ_VPATH 1 // pop128's sift-down path by per-lane ancestor masks (0: scalar walk)
 #endif
@@ -488,6 +494,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // prediction can skip links back to nodes already expanded before the visited test has answered
         uint32_t popped_bits = 0u;
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
+        // DRM_PQ_AHEAD: node pn's row (v1n), distances (dalln) and visited words (vwn, in flight) were prepared
+        // during the previous hop; pred / v1_pref / c8_pref then hold the node after it
+        constexpr bool AH = INL && DRM_PQ_AHEAD;
+        int32_t pn = -1, v1n = -1;
+        uint32_t dalln = 0xFFFFFFFFu, vwn = 0xFFFFFFFFu;
         while (nvalid > 0) {
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
@@ -522,20 +533,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             DRM_FSTAMP(2);
 
             // expand v0's level-0 row (one coalesced load, lane j = link j)
+            const bool hit2 = AH && v0 == pn; // row, distances and visited words all prepared
+            const bool hit = !hit2 && v0 == pred;
             int32_t v1 = v1_pref;
-            const bool hit = v0 == pred;
+            if (AH) {
+                // each path reads only registers that are ready on it: the wait for a pending row load stays
+                // inside its own branch, so the two-ahead path does not wait here for the loads it issued
+                // during the previous hop (the next test's words, the row after)
+                if (hit2) {
+                    v1 = v1n;
+                } else if (hit) {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    v1 = v1_pref;
+                }
+            }
             if (STAMPS) { // row prediction hits / hops
-                st_acc[8] += hit ? 1u : 0u;
+                st_acc[8] += (hit || hit2) ? 1u : 0u;
                 st_acc[9] += 1u;
+                st_acc[10] += hit2 ? 1u : 0u;
             }
             if (INL) {
                 const uint32_t h0 = pop_hash(v0);
                 if (lane == (int)((h0 >> 5) & 63u))
                     popped_bits |= 1u << (h0 & 31u);
-                if (!hit) {
+                if (!hit && !hit2) {
                     const int32_t *row = a.rows + (size_t)v0 * (size_t)a.row_words;
                     v1 = lane < deg0 ? row[lane] : -1;
                     c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(row + deg0)[lane] : make_uint2(0u, 0u);
+                    if (AH)
+                        __builtin_amdgcn_s_waitcnt(0);
                 }
             } else if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
@@ -548,6 +574,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const uint32_t bit = 1u << (v1 & 31);
             const bool use_spec = !INL && DRM_PQ_SPEC && hit && spec;
             if (INL) {
+                if (!hit2) {
                 c8 = c8_pref; // arrived with the row
                 // the visited test is in flight while the distances are formed. DRM_PQ_VIS_LOAD: a plain L2 load
                 // (sc1: this wave's own earlier marks are at L2, never in its L1), and only the fresh links are
@@ -557,6 +584,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if (act)
                     old = DRM_PQ_VIS_LOAD ? __hip_atomic_load(&vis[v1 >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                           : vis_test_set(&vis[v1 >> 5], bit);
+                }
             } else if (use_spec) {
                 c8 = c8_pref;
                 old = act ? vw_pref : 0xFFFFFFFFu;
@@ -565,7 +593,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 old = vis_test_set(&vis[v1 >> 5], bit);
             }
             uint32_t dall = 0xFFFFFFFFu;
-            if (INL) {
+            if (AH && hit2) {
+                old = act ? vwn : 0xFFFFFFFFu;
+                dall = dalln;
+            } else if (INL) {
                 // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min:
                 // the smallest valid heap slot or active link not known to be popped; its row (ids + codes) is
                 // fetched now, beside the visited test
@@ -653,6 +684,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     clr[p] = v1;
             }
             clear_n += nf;
+            if (AH) {
+                // two ahead: the predicted next row (pred, fetched above or during the previous hop) gets its
+                // visited test now -- after this hop's marks, and before anything else marks the bitmap, so the
+                // words it returns are the ones the next hop would load -- and its distances; then the node
+                // after it is predicted (smallest of the heap's valid slots, this hop's fresh links and the next
+                // row's links not known to be popped, the next node itself excluded) and its row is fetched
+                pn = -1;
+                if (pred >= 0) {
+                    const int32_t vx = v1_pref;
+                    const uint2 cx = c8_pref;
+                    const uint64_t negx = ballot(vx < 0) & deg0m;
+                    const int jx = negx ? __builtin_ctzll(negx) : deg0;
+                    const bool ax = lane < jx;
+                    vwn = 0xFFFFFFFFu;
+                    if (ax)
+                        vwn = __hip_atomic_load(&vis[vx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    float lv[8];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        lv[m] = lut[m * 256 + ((cx.x >> (8 * m)) & 255u)];
+                        lv[m + 4] = lut[(m + 4) * 256 + ((cx.y >> (8 * m)) & 255u)];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    float r = 0.0f;
+#pragma unroll
+                    for (int m = 0; m < 8; ++m)
+                        r = __fadd_rn(r, lv[m]);
+                    dalln = ord32(r);
+                    const uint32_t hv = pop_hash(vx);
+                    const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
+                    const bool kp = (pw >> (hv & 31u)) & 1u;
+                    const uint32_t dx = (ax && !kp && vx != pred) ? dalln : 0xFFFFFFFFu;
+                    const uint32_t df = v1 != pred ? dk : 0xFFFFFFFFu;
+                    const uint32_t hL = (lo32(hp.L) != kPopLo && unpack_id(hp.L) != pred) ? hi32(hp.L) : 0xFFFFFFFFu;
+                    const uint32_t hR = (lo32(hp.R) != kPopLo && unpack_id(hp.R) != pred) ? hi32(hp.R) : 0xFFFFFFFFu;
+                    uint32_t mk = dx < df ? dx : df;
+                    mk = mk < hL ? mk : hL;
+                    mk = mk < hR ? mk : hR;
+                    const int32_t mid = dx == mk ? vx : (df == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R)));
+                    const uint32_t mm = wave_min_u32(mk);
+                    pn = pred;
+                    v1n = vx;
+                    pred = -1;
+                    if (mm != 0xFFFFFFFFu) {
+                        pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
+                        const int32_t *prow = a.rows + (size_t)pred * (size_t)a.row_words;
+                        v1_pref = lane < deg0 ? prow[lane] : -1;
+                        c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(prow + deg0)[lane] : make_uint2(0u, 0u);
+                    }
+                }
+            }
             DRM_FSTAMP(4);
             // add_to_heap for each fresh link in row order. On a full heap the root distance only
             // falls, so a link at or above it now is rejected for the whole row: it is skipped here. It cannot
