@@ -83,7 +83,8 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 void free_index(drm::DeviceIndex &d)
 {
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
-                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes};
+                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes,
+                    d.vis_tag,    d.vis_gen};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -310,6 +311,26 @@ int drm_debug_search_stamps(drm_index *index, uint64_t *out12)
             throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
         DRM_HIP_CHECK(hipMemcpy(out12, index->dev.stamps, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
         DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 12 * sizeof(uint64_t)));
+    });
+}
+
+// Test hook: restart every slot's visited words at the given generation (the inline-row kernel's tag), e.g. just
+// below the 16-bit wrap, so that a test sees the slots zero their words mid-batch
+int drm_debug_search_generation(drm_index *index, uint32_t generation)
+{
+    return guarded([&] {
+        if (!index || !index->dev.vis_gen)
+            throw Error(DRM_ERR_ARG, "index has no tagged visited words (inline rows off)");
+        if (generation > 0xFFFFu)
+            throw Error(DRM_ERR_ARG, "generation must be <= 0xFFFF");
+        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
+        DRM_HIP_CHECK(hipDeviceSynchronize());
+        // generations only ever increase between wraps: a word's tag must never reappear for a later query, so
+        // the words restart from zero with the new generation
+        DRM_HIP_CHECK(hipMemset(index->dev.vis_tag, 0,
+                                sizeof(uint32_t) * (size_t)index->dev.tag_slots * (size_t)index->dev.tag_words));
+        std::vector<uint32_t> g((size_t)index->dev.tag_slots, generation);
+        DRM_HIP_CHECK(hipMemcpy(index->dev.vis_gen, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     });
 }
 

@@ -83,6 +83,13 @@ struct DeviceIndex {
     uint64_t *log = nullptr;       // [n_slots][log_cap] accepted pushes (lean kernel, k == ef)
     int32_t log_cap = 0, log_slots = 0;
     int32_t log_cap_req = 2048;    // entries per slot (DRM_SEARCH_LOG_CAP; >= ef + 64, compaction beyond)
+    // inline-row lean kernel: generation-tagged visited words, 16 node bits | (query generation << 16) each,
+    // never cleared per query (a new generation per query; a slot zeroes its words at the 16-bit wrap). The
+    // plain bitmap above is then allocated only if another kernel runs
+    int32_t tag_slots = 0;
+    int64_t tag_words = 0;         // words per slot: ceil(ntotal / 16), a multiple of 4
+    uint32_t *vis_tag = nullptr;   // [tag_slots][tag_words]
+    uint32_t *vis_gen = nullptr;   // [tag_slots] each slot's last generation
     int64_t device_bytes = 0;
     HnswPqHost meta; // header fields kept for drm_index_get_info (vectors released)
 };
@@ -123,6 +130,7 @@ struct SearchArgs {
     const int32_t *rows;   // lean kernel, inline layout: [ntotal][row_words] ids + codes (DeviceIndex::rows)
     int32_t row_words;
     const uint2 *upper_codes; // lean kernel, inline layout: codes beside upper_nbr (DeviceIndex::upper_codes)
+    uint32_t *vis_gen;        // lean kernel, inline layout: per-slot generations; `visited` is then vis_tag
 };
 
 // lean kernel (hnsw_pq_fast.hip): PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64

@@ -56,6 +56,19 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src)
 {
     return ((uint64_t)bperm32(hi32(v), src) << 32) | bperm32(lo32(v), src);
 }
+__device__ __forceinline__ uint64_t bperm64_addr(uint64_t v, uint32_t addr) // addr = source lane * 4
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)hi32(v)) << 32) |
+           (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)lo32(v));
+}
+// a wave-uniform lane mask as this lane's predicate, with no per-lane arithmetic (the select uses the mask)
+__device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// a > b for wave-uniform u64 keys, on the scalar unit (two 32-bit compares)
+__device__ __forceinline__ bool sgt64(uint64_t a, uint64_t b)
+{
+    const uint32_t ah = hi32(a), bh = hi32(b);
+    return ah > bh || (ah == bh && lo32(a) > lo32(b));
+}
 __device__ __forceinline__ int bitlen(uint32_t x) { return 32 - __builtin_clz(x); } // x >= 1
 __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // lane i <- lane i-1
 {
@@ -64,11 +77,60 @@ __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // la
     return ((uint64_t)h << 32) | o;
 }
 
-#ifndef DRM_PQ_AHEAD
-// INL: the visited test of the predicted next row is issued before this hop's push loop, and the row after
-// that is predicted and fetched then too (two hops ahead), so the test's round trip overlaps the push loop
-#define DRM_PQ_AHEAD 0
+// byte M of c times 4 (the LUT entry's byte offset within its sub-quantizer row) in one SDWA shift
+template <int M>
+__device__ __forceinline__ uint32_t bx4(uint32_t c)
+{
+    uint32_t r;
+    if constexpr (M == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(c));
+    else if constexpr (M == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(c));
+    else if constexpr (M == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(c));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(c));
+    return r;
+}
+
+// PQ-ADC distance of one 8-byte code per lane: the 8 LUT reads (sub-quantizer m at byte offset m * 1024) all in
+// flight before the first add, then the adds in sub-quantizer order (distance_to_code, 0 ulp vs the oracle)
+__device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
+{
+    const char *b = reinterpret_cast<const char *>(lut);
+    float lv[8];
+    lv[0] = *reinterpret_cast<const float *>(b + bx4<0>(c.x));
+    lv[1] = *reinterpret_cast<const float *>(b + bx4<1>(c.x) + 1024);
+    lv[2] = *reinterpret_cast<const float *>(b + bx4<2>(c.x) + 2048);
+    lv[3] = *reinterpret_cast<const float *>(b + bx4<3>(c.x) + 3072);
+    lv[4] = *reinterpret_cast<const float *>(b + bx4<0>(c.y) + 4096);
+    lv[5] = *reinterpret_cast<const float *>(b + bx4<1>(c.y) + 5120);
+    lv[6] = *reinterpret_cast<const float *>(b + bx4<2>(c.y) + 6144);
+    lv[7] = *reinterpret_cast<const float *>(b + bx4<3>(c.y) + 7168);
+    __builtin_amdgcn_sched_barrier(0);
+    float r = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+        r = __fadd_rn(r, lv[m]);
+    return ord32(r);
+}
+
+#ifndef DRM_PQ_HEAPV2
+#define DRM_PQ_HEAPV2 1 // pop128v2 / push128v2 (requires DRM_PQ_SROOT)
 #endif
+
+#ifndef DRM_PQ_TAGMARK
+// tagged visited words, first mark of a word in a query: 1 = atomic max (generation) then OR (the bit);
+// 0 = plain store then OR (measured 3.7x slower: a store and an atomic to one address back to back);
+// 2 = OR only (diagnostic: wrong once a word carries an older generation)
+#define DRM_PQ_TAGMARK 1
+#endif
+
+#ifndef DRM_PQ_SROOT
+// ef = 128 replace pushes keep the root (slot 0) in scalar registers only; lane 63's R is refreshed once per hop
+#define DRM_PQ_SROOT 1
+#endif
+
 
 #ifndef DRM_PQ_VPATH
 #define DRM_PQ_VPATH 1 // pop128's sift-down path by per-lane ancestor masks (0: scalar walk)
@@ -77,9 +139,21 @@ __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // la
 // Per-lane constants of node p = lane: A = p and its ancestors, Aup = its ancestors, Lreq = the
 // ancestors whose path toward p takes the left child (2a + 1).
 struct PathConst {
-    uint64_t A, Aup, Lreq;
-    __device__ explicit PathConst(int lane) : A(1ull << lane), Aup(0), Lreq(0)
+    // every ancestor of any lane p (< 64) is below lane 32, so A's, Aup's and Lreq's high halves hold at most p
+    // itself: only the low halves are kept (three VGPRs), and p's own bit is checked against the ballot mask
+    uint32_t Alo, Auplo, Lreqlo;
+    // ds_bpermute byte addresses: this lane's left / right child lane (slots 2p+1, 2p+2 are held by lanes
+    // 2p+1, 2p+2 mod 64), and its parent in the chain of slot 127's ancestors (lane >> 1)
+    uint32_t addrL, addrR, addrHalf;
+    // heap filling (push_fill): this lane's slots 2p+1, 2p+2 as 1-based positions 2p+2, 2p+3 share the bit
+    // length bl; their father is slot p, held by lane (p-1)/2 (the L half when p is odd; the root for p = 0)
+    uint32_t c2, bl, addrF;
+    __device__ explicit PathConst(int lane)
+        : addrL((uint32_t)((2 * lane + 1) & 63) << 2), addrR((uint32_t)((2 * lane + 2) & 63) << 2),
+          addrHalf((uint32_t)(lane >> 1) << 2), c2(2u * (uint32_t)lane + 2u), bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)),
+          addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 0u)
     {
+        uint64_t A = 1ull << lane, Aup = 0, Lreq = 0;
         for (int c = lane; c > 0;) {
             const int a = (c - 1) >> 1;
             A |= 1ull << a;
@@ -88,6 +162,15 @@ struct PathConst {
                 Lreq |= 1ull << a;
             c = a;
         }
+        Alo = (uint32_t)A;
+        Auplo = (uint32_t)Aup;
+        Lreqlo = (uint32_t)Lreq;
+    }
+    // the lanes on the sift-down path: p and all its ancestors have mv set, and every ancestor chose the child
+    // toward p (lm: the nodes that take their L child)
+    __device__ __forceinline__ uint64_t path(uint64_t mv, uint64_t lm) const
+    {
+        return ballot(((uint32_t)mv & Alo) == Alo) & (mv | 0xFFFFFFFFull) & ballot(((uint32_t)lm & Auplo) == Lreqlo);
     }
 };
 
@@ -157,7 +240,7 @@ struct Heap {
         // node p is on the sift-down path (its chosen child moves up) iff p and all its ancestors have
         // mv set and every ancestor chose the child toward p: one test per lane against its constant
         // ancestor masks, instead of a 7-step scalar walk
-        const uint64_t W = ballot((mv & pc.A) == pc.A) & ballot((lm & pc.Aup) == pc.Lreq);
+        const uint64_t W = pc.path(mv, lm);
         uint32_t hole = 0;
         if (W) {
             const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
@@ -181,7 +264,7 @@ struct Heap {
         if (writer && !takeL)
             R = nv;
         const uint64_t rootv = (W & 1ull) ? readlane64(chv, 0) : val;
-        if (lane == 63)
+        if (!DRM_PQ_SROOT && lane == 63)
             R = rootv;
         return rootv;
     }
@@ -196,17 +279,109 @@ struct Heap {
         const bool holderL = lane == 63 || (lane < 32 && ((lane + 1) & lane) == 0); // slots 127, 63, ..., 1
         // ancestors of slot 127: the L halves of lanes 0, 1, 3, 7, 15, 31 and lane 63 (its R is the root)
         constexpr uint64_t kAnc = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
+#if DRM_PQ_SROOT
+        // the root is rootv (scalar); lane 63's R is stale until the hop refreshes it
+        constexpr uint64_t kAncL = kAnc & ~(1ull << 63);
+        const int h = __builtin_popcountll(ballot(val > L) & kAncL) + (val > rootv ? 1 : 0);
+#else
         const uint64_t av = lane == 63 ? R : L;
         const int h = __builtin_popcountll(ballot(val > av) & kAnc);
+#endif
         const uint64_t fl = bperm64(L, lane >> 1);
         const uint64_t srcv = lane == 0 ? rootv : fl;
         const int m = 7 - bitlen((uint32_t)lane + 1u);
         if (holderL && m <= h)
             L = m < h ? srcv : val;
-        if (h == 7 && lane == 63)
+        if (!DRM_PQ_SROOT && h == 7 && lane == 63)
             R = val;
         return h == 7 ? val : rootv;
     }
+
+#if DRM_PQ_HEAPV2
+    // pop128 with lane-mask predicates (DRM_PQ_HEAPV2): the same sift-down as pop128, with the path's lanes
+    // selected by their ballot masks (no per-lane mask arithmetic), and the last path node fetching the sifted
+    // value from lane 63 (slot 127 = val: lane 63 always takes its L) in the same ds_bpermute that moves the
+    // other children up. Lane 63's R (the root) is left stale (DRM_PQ_SROOT); returns the new root.
+    __device__ __forceinline__ uint64_t pop128v2(const PathConst &pc)
+    {
+        const uint64_t val = readlane64(L, 63);
+        const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child
+        const bool takeL = in_mask(lm);
+        const uint64_t chv = takeL ? L : R;
+        const uint64_t mv = ballot(!(val > chv));         // the chosen child moves up
+        const uint64_t W = pc.path(mv, lm);
+        if (!W)
+            return val; // the root's chosen child stays: val becomes the root
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
+        uint32_t addr = takeL ? pc.addrL : pc.addrR;
+        addr = in_mask(1ull << last) ? (63u << 2) : addr;
+        const uint64_t up = bperm64_addr(chv, addr);
+        L = in_mask(W & lm) ? up : L;
+        R = in_mask(W & ~lm) ? up : R;
+        return (W & 1ull) ? readlane64(chv, 0) : val;
+    }
+
+    // push128 with lane-mask predicates: the chain holders below the insertion height take their fathers'
+    // values (one ds_bpermute from lane >> 1; slot 1 takes the root), the slot at the height takes val
+    __device__ __forceinline__ uint64_t push128v2(uint64_t val, const PathConst &pc, uint64_t rootv)
+    {
+        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
+        constexpr uint64_t kAncL = kHold & ~(1ull << 63); // slots 63, 31, 15, 7, 3, 1 (the root is rootv)
+        const int h = __builtin_popcountll(ballot(val > L) & kAncL) + (sgt64(val, rootv) ? 1 : 0);
+        const uint64_t fl = bperm64_addr(L, pc.addrHalf);
+        if (h == 0) { // val stays at slot 127
+            L = in_mask(1ull << 63) ? val : L;
+            return rootv;
+        }
+        // holders with chain index m = 7 - bitlen(lane + 1) < h: lanes >= 2^(7-h) - 1
+        const uint64_t mlt = kHold & (~0ull << ((1u << (7 - h)) - 1u));
+        L = in_mask(mlt) ? fl : L;
+        if (h == 7) { // val becomes the root; the old root moves down to slot 1 (lane 0)
+            L = in_mask(1ull) ? rootv : L;
+            return val;
+        }
+        L = in_mask(1ull << ((1u << (6 - h)) - 1u)) ? val : L; // the chain slot at index h
+        return rootv;
+    }
+
+    // faiss heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128): val enters slot s = k - 1 and
+    // sifts up its ancestors, slot (k >> m) - 1 at chain index m (the root at m = bitlen(k) - 1). Lane-mask
+    // form: each lane tests whether one of its halves is on the chain (both halves share the index), the
+    // ancestors below val are a bottom prefix of length h (heap order), the slots of index < h take their
+    // father's value (two ds_bpermute per half), and the slot of index h takes val. The root is rootv (scalar;
+    // lane 63's R is left stale); returns the new root.
+    __device__ __forceinline__ uint64_t push_fill_v2(int k, uint64_t val, const PathConst &pc, uint64_t rootv)
+    {
+        const uint32_t s1 = (uint32_t)k;
+        const int B = bitlen(s1);
+        const int m = B - (int)pc.bl;
+        const uint32_t t = m >= 0 ? (s1 >> m) : 0u;
+        const uint64_t OL = ballot(t == pc.c2), OR = ballot(t == pc.c2 + 1u); // this lane's half on the chain
+        const uint32_t sl = (s1 - 2u) >> 1;                                     // the lane of slot s
+        const uint64_t selfL = (s1 & 1u) ? 0ull : (1ull << sl), selfR = (s1 & 1u) ? (1ull << sl) : 0ull;
+        const int h = __builtin_popcountll(ballot(val > L) & OL & ~selfL) + __builtin_popcountll(ballot(val > R) & OR & ~selfR) +
+                      (sgt64(val, rootv) ? 1 : 0);
+        if (h > 0) {
+            const uint64_t fL = bperm64_addr(L, pc.addrF), fR = bperm64_addr(R, pc.addrF);
+            const uint64_t f = in_mask(0xAAAAAAAAAAAAAAAAull) ? fL : fR; // father slot p odd: an L half
+            const uint64_t mlt = ~0ull << ((1u << (B - h - 1)) - 1u);        // chain index < h: bl > B - h
+            L = in_mask(OL & mlt) ? f : L;
+            R = in_mask(OR & mlt) ? f : R;
+            if (h == B - 1) { // val becomes the root; the old root moves to its child on the chain (lane 0)
+                L = in_mask(OL & 1ull) ? rootv : L;
+                R = in_mask(OR & 1ull) ? rootv : R;
+                return val;
+            }
+        }
+        const uint32_t x = (s1 >> h) - 1u; // the slot of chain index h (>= 1 here)
+        const uint64_t xb = 1ull << ((x - 1u) >> 1);
+        if (x & 1u)
+            L = in_mask(xb) ? val : L;
+        else
+            R = in_mask(xb) ? val : R;
+        return rootv;
+    }
+#endif
 
     // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
     __device__ __forceinline__ void push(int k, uint64_t val, int lane)
@@ -399,7 +574,9 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
 template <bool LOGRES, bool STAMPS, bool FIX128, bool INL = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
 {
-    extern __shared__ __align__(16) unsigned char smem[];
+    // the 8 x 256 f32 LUT (the kernel's only LDS): a static allocation at LDS address 0, so the LUT reads
+    // address it with no base add
+    __shared__ __align__(16) unsigned char smem[8 * 256 * sizeof(float)];
     uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
@@ -414,6 +591,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     const PathConst pconst(lane);
     const uint64_t deg0m = deg0 >= 64 ? ~0ull : ((1ull << deg0) - 1ull); // lanes holding a link slot
     const uint32_t kInfKey = ord32(INFINITY);
+    // INL: this slot's query generation (the tag of its visited words), carried across launches
+    uint32_t gen = INL ? a.vis_gen[blockIdx.x] : 0u;
 
     for (;;) {
         int q = 0;
@@ -422,6 +601,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         q = __builtin_amdgcn_readfirstlane(q);
         if ((int64_t)q >= a.n)
             break;
+        if (INL) { // a new generation per query; at the 16-bit wrap the slot's words restart from zero
+            gen += 1u;
+            if (gen > 0xFFFFu) {
+                uint4 *v4 = reinterpret_cast<uint4 *>(vis);
+                for (int64_t w = lane; w < a.vis_words / 4; w += 64)
+                    v4[w] = make_uint4(0u, 0u, 0u, 0u);
+                gen = 1u;
+            }
+        }
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < k; j += 64) {
                 a.D[(int64_t)q * k + j] = INFINITY;
@@ -476,8 +664,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 add_result(root);
         }
         if (lane == 0) {
-            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
-            if (a.clear_cap > 0)
+            if (INL) // the query's first mark: the word's generation is an older one
+                __hip_atomic_store(&vis[nearest >> 4], (gen << 16) | (1u << (nearest & 15)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
+            if (!INL && a.clear_cap > 0)
                 clr[0] = nearest;
         }
         int clear_n = 1;
@@ -494,17 +686,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // prediction can skip links back to nodes already expanded before the visited test has answered
         uint32_t popped_bits = 0u;
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
-        // DRM_PQ_AHEAD: node pn's row (v1n), distances (dalln) and visited words (vwn, in flight) were prepared
-        // during the previous hop; pred / v1_pref / c8_pref then hold the node after it
-        constexpr bool AH = INL && DRM_PQ_AHEAD;
-        int32_t pn = -1, v1n = -1;
-        uint32_t dalln = 0xFFFFFFFFu, vwn = 0xFFFFFFFFu;
         while (nvalid > 0) {
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
             // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest
-            const bool pickR = lane != 63 ? cR <= cL : cR < cL;
+            const bool pickR = cR < cL || (cR == cL && lane != 63); // lane masks, no per-lane selects
             const uint32_t pk = pickR ? cR : cL;
             const uint32_t d0 = wave_min_u32(pk);
             const uint64_t rightm = ballot(pickR);
@@ -532,36 +719,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 break;
             DRM_FSTAMP(2);
 
+            int32_t v1;
+            uint32_t dk;
+            uint64_t fm;
             // expand v0's level-0 row (one coalesced load, lane j = link j)
-            const bool hit2 = AH && v0 == pn; // row, distances and visited words all prepared
-            const bool hit = !hit2 && v0 == pred;
-            int32_t v1 = v1_pref;
-            if (AH) {
-                // each path reads only registers that are ready on it: the wait for a pending row load stays
-                // inside its own branch, so the two-ahead path does not wait here for the loads it issued
-                // during the previous hop (the next test's words, the row after)
-                if (hit2) {
-                    v1 = v1n;
-                } else if (hit) {
-                    __builtin_amdgcn_s_waitcnt(0);
-                    v1 = v1_pref;
-                }
-            }
+            v1 = v1_pref;
+            const bool hit = v0 == pred;
             if (STAMPS) { // row prediction hits / hops
-                st_acc[8] += (hit || hit2) ? 1u : 0u;
+                st_acc[8] += hit ? 1u : 0u;
                 st_acc[9] += 1u;
-                st_acc[10] += hit2 ? 1u : 0u;
             }
             if (INL) {
                 const uint32_t h0 = pop_hash(v0);
                 if (lane == (int)((h0 >> 5) & 63u))
                     popped_bits |= 1u << (h0 & 31u);
-                if (!hit && !hit2) {
+                if (!hit) {
                     const int32_t *row = a.rows + (size_t)v0 * (size_t)a.row_words;
                     v1 = lane < deg0 ? row[lane] : -1;
                     c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(row + deg0)[lane] : make_uint2(0u, 0u);
-                    if (AH)
-                        __builtin_amdgcn_s_waitcnt(0);
                 }
             } else if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
@@ -571,20 +746,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const uint64_t actm = jmax >= 64 ? ~0ull : ((1ull << jmax) - 1ull);
             uint2 c8 = make_uint2(0u, 0u);
             uint32_t old = 0xFFFFFFFFu;
-            const uint32_t bit = 1u << (v1 & 31);
+            // INL: tagged words (16 node bits | generation << 16); else the plain bitmap (32 node bits)
+            const uint32_t bit = INL ? 1u << (v1 & 15) : 1u << (v1 & 31);
             const bool use_spec = !INL && DRM_PQ_SPEC && hit && spec;
             if (INL) {
-                if (!hit2) {
                 c8 = c8_pref; // arrived with the row
-                // the visited test is in flight while the distances are formed. DRM_PQ_VIS_LOAD: a plain L2 load
-                // (sc1: this wave's own earlier marks are at L2, never in its L1), and only the fresh links are
-                // marked afterwards -- a test-and-set on every link dirtied a bitmap sector per link, visited or
-                // not. Exact: this wave alone writes its bitmap, its earlier marks were issued before this load,
-                // and a repeated id in one row is fresh once (check_dups below) and so marked once.
+                // the visited test is in flight while the distances are formed: a plain L2 load (sc1: this wave's
+                // own earlier marks are at L2, never in its L1), and only the fresh links are marked afterwards.
+                // Exact: this wave alone writes its words, its earlier marks were issued before this load, and a
+                // repeated id in one row is fresh once (check_dups below) and so marked once.
                 if (act)
-                    old = DRM_PQ_VIS_LOAD ? __hip_atomic_load(&vis[v1 >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : vis_test_set(&vis[v1 >> 5], bit);
-                }
+                    old = __hip_atomic_load(&vis[v1 >> 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (use_spec) {
                 c8 = c8_pref;
                 old = act ? vw_pref : 0xFFFFFFFFu;
@@ -593,25 +765,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 old = vis_test_set(&vis[v1 >> 5], bit);
             }
             uint32_t dall = 0xFFFFFFFFu;
-            if (AH && hit2) {
-                old = act ? vwn : 0xFFFFFFFFu;
-                dall = dalln;
-            } else if (INL) {
+            if (INL) {
                 // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min:
                 // the smallest valid heap slot or active link not known to be popped; its row (ids + codes) is
                 // fetched now, beside the visited test
-                float lv[8];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    lv[m] = lut[m * 256 + ((c8.x >> (8 * m)) & 255u)];
-                    lv[m + 4] = lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                float r = 0.0f;
-#pragma unroll
-                for (int m = 0; m < 8; ++m)
-                    r = __fadd_rn(r, lv[m]);
-                dall = ord32(r);
+                dall = adc8(lut, c8);
                 const uint32_t hv = pop_hash(v1);
                 const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
                 const bool known_popped = (pw >> (hv & 31u)) & 1u;
@@ -630,7 +788,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(prow + deg0)[lane] : make_uint2(0u, 0u);
                 }
             }
-            bool fresh = act && (old & bit) == 0u;
+            // visited in this query: (tagged) the word carries this query's generation and the node's bit
+            const bool seen = INL ? ((old >> 16) == gen && (old & bit) != 0u) : (old & bit) != 0u;
+            bool fresh = act && !seen;
             if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
                     const int32_t vj = __shfl(v1, j, 64);
@@ -638,16 +798,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         fresh = false;
                 }
             }
-            if ((use_spec || (INL && DRM_PQ_VIS_LOAD)) && fresh) // the test was a load: mark the
-                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); // fresh links
+            if (INL && fresh) {
+                // mark the fresh links: a word still carrying an older generation is restarted with this one
+                // (atomic max with gen << 16: generations only grow between wraps, so the max drops the old tag
+                // and bits), then every fresh link ORs in its bit; both atomics of a lane go to one address in
+                // order, and lanes sharing a word all OR their bits after it restarted, so no bit is lost
+                const uint32_t tagbit = (gen << 16) | bit;
+#if DRM_PQ_TAGMARK == 0
+                if ((old >> 16) != gen)
+                    __hip_atomic_store(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#elif DRM_PQ_TAGMARK == 1
+                if ((old >> 16) != gen)
+                    __hip_atomic_fetch_max(&vis[v1 >> 4], gen << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+                __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (use_spec && fresh) // the test was a load: mark the fresh links
+                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             DRM_FSTAMP(3);
-            const uint64_t fm = check_dups ? ballot(fresh) : ballot((old & bit) == 0u) & actm;
+            fm = check_dups ? ballot(fresh) : ballot(!seen) & actm;
             const int nf = __builtin_popcountll(fm);
             ndis0 += nf;
             // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
             // on the fresh ones)
             // all 8 LDS reads in flight before the first add (the adds stay in sub-quantizer order)
-            uint32_t dk;
             if (INL) {
                 dk = fresh ? dall : 0xFFFFFFFFu;
             } else {
@@ -678,69 +851,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     v1_pref = lane < deg0 ? a.nbr0[(size_t)pred * (size_t)deg0 + lane] : -1;
                 }
             }
-            if (fresh) { // VisitedTable::advance list (stored after the loads above)
+            if (!INL && fresh) { // VisitedTable::advance list (stored after the loads above)
                 const int p = clear_n + __builtin_popcountll(fm & lanes_below(lane));
                 if (p < a.clear_cap)
                     clr[p] = v1;
             }
             clear_n += nf;
-            if (AH) {
-                // two ahead: the predicted next row (pred, fetched above or during the previous hop) gets its
-                // visited test now -- after this hop's marks, and before anything else marks the bitmap, so the
-                // words it returns are the ones the next hop would load -- and its distances; then the node
-                // after it is predicted (smallest of the heap's valid slots, this hop's fresh links and the next
-                // row's links not known to be popped, the next node itself excluded) and its row is fetched
-                pn = -1;
-                if (pred >= 0) {
-                    const int32_t vx = v1_pref;
-                    const uint2 cx = c8_pref;
-                    const uint64_t negx = ballot(vx < 0) & deg0m;
-                    const int jx = negx ? __builtin_ctzll(negx) : deg0;
-                    const bool ax = lane < jx;
-                    vwn = 0xFFFFFFFFu;
-                    if (ax)
-                        vwn = __hip_atomic_load(&vis[vx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    float lv[8];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        lv[m] = lut[m * 256 + ((cx.x >> (8 * m)) & 255u)];
-                        lv[m + 4] = lut[(m + 4) * 256 + ((cx.y >> (8 * m)) & 255u)];
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    float r = 0.0f;
-#pragma unroll
-                    for (int m = 0; m < 8; ++m)
-                        r = __fadd_rn(r, lv[m]);
-                    dalln = ord32(r);
-                    const uint32_t hv = pop_hash(vx);
-                    const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
-                    const bool kp = (pw >> (hv & 31u)) & 1u;
-                    const uint32_t dx = (ax && !kp && vx != pred) ? dalln : 0xFFFFFFFFu;
-                    const uint32_t df = v1 != pred ? dk : 0xFFFFFFFFu;
-                    const uint32_t hL = (lo32(hp.L) != kPopLo && unpack_id(hp.L) != pred) ? hi32(hp.L) : 0xFFFFFFFFu;
-                    const uint32_t hR = (lo32(hp.R) != kPopLo && unpack_id(hp.R) != pred) ? hi32(hp.R) : 0xFFFFFFFFu;
-                    uint32_t mk = dx < df ? dx : df;
-                    mk = mk < hL ? mk : hL;
-                    mk = mk < hR ? mk : hR;
-                    const int32_t mid = dx == mk ? vx : (df == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R)));
-                    const uint32_t mm = wave_min_u32(mk);
-                    pn = pred;
-                    v1n = vx;
-                    pred = -1;
-                    if (mm != 0xFFFFFFFFu) {
-                        pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
-                        const int32_t *prow = a.rows + (size_t)pred * (size_t)a.row_words;
-                        v1_pref = lane < deg0 ? prow[lane] : -1;
-                        c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(prow + deg0)[lane] : make_uint2(0u, 0u);
-                    }
-                }
-            }
             DRM_FSTAMP(4);
             // add_to_heap for each fresh link in row order. On a full heap the root distance only
             // falls, so a link at or above it now is rejected for the whole row: it is skipped here. It cannot
             // enter a k < ef result set either: the heap keeps the ef smallest pushed keys (popped slots keep
             // theirs), so its root is at or above the k-th smallest result, the threshold add_result tests.
             uint64_t rem = fm, accm = 0;
+            bool replaced = false;
             if (kc == ef)
                 rem &= ballot(dk < hi32(root));
             while (rem) {
@@ -758,7 +881,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (lo32(root) != kPopLo)
                         --nvalid;
                     if (ef == 128) {
+#if DRM_PQ_HEAPV2
+                        root = hp.push128v2(val, pconst, hp.pop128v2(pconst));
+#else
                         root = hp.push128(val, lane, hp.pop128(lane, pconst));
+#endif
+                        replaced = true;
+                        if (STAMPS)
+                            st_acc[11] += 1u;
                     } else {
                         hp.pop(kc, lane);
                         hp.push(kc, val, lane);
@@ -766,12 +896,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     }
                 } else {
                     ++kc;
-                    hp.push(kc, val, lane);
-                    root = readlane64(hp.R, 63);
+#if DRM_PQ_HEAPV2
+                    if (ef == 128) {
+                        root = hp.push_fill_v2(kc, val, pconst, root);
+                        replaced = true;
+                    } else
+#endif
+                    {
+                        hp.push(kc, val, lane);
+                        root = readlane64(hp.R, 63);
+                    }
                 }
                 ++nvalid;
                 accm |= 1ull << l;
             }
+            if (DRM_PQ_SROOT && replaced && lane == 63)
+                hp.R = root;
             if (LOGRES && accm) {
                 const int na = __builtin_popcountll(accm);
                 if (logn + na > a.log_cap) {
@@ -839,18 +979,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (a.nhops_upper)
                 a.nhops_upper[q] = nhops_upper;
         }
-        // VisitedTable::advance: clear exactly the bits this query set
-        if (clear_n <= a.clear_cap) {
+        // VisitedTable::advance: clear exactly the bits this query set (INL: nothing to clear, the next query
+        // has a new generation)
+        if (INL) {
+        } else if (clear_n <= a.clear_cap) {
             for (int t = lane; t < clear_n; t += 64)
                 vis[clr[t] >> 5] = 0u;
         } else {
             for (int64_t w = lane; w < a.vis_words; w += 64)
                 vis[w] = 0u;
         }
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
+        if (!INL) { // the clears land before the next query's tests
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        }
         DRM_FSTAMP(6);
     }
+    if (INL && lane == 0)
+        a.vis_gen[blockIdx.x] = gen;
     if (STAMPS && lane == 0 && a.stamps)
         for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
@@ -923,33 +1069,36 @@ bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream)
 {
+    (void)lds; // static LDS (the LUT)
     const bool logres = a.k == a.ef;
     const bool fix = a.ef == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
     const bool inl = a.rows != nullptr;
-    if (fix && logres && inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true, true>), dim3(slots), dim3(64), lds, stream, a);
+    if (stamps && inl && logres && a.ef == 128 && a.efSearch == 128 && !a.check_dups)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, true, true>), dim3(slots), dim3(64), 0, stream, a);
+    else if (fix && logres && inl)
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (fix && inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (inl && logres && stamps)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (inl && logres)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (fix && logres)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (fix)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true>), dim3(slots), dim3(64), 0, stream, a);
     else if (logres) {
         if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false>), dim3(slots), dim3(64), 0, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false>), dim3(slots), dim3(64), 0, stream, a);
     } else {
         if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true, false>), dim3(slots), dim3(64), 0, stream, a);
         else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false>), dim3(slots), dim3(64), lds, stream, a);
+            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false>), dim3(slots), dim3(64), 0, stream, a);
     }
     DRM_HIP_CHECK(hipGetLastError());
 }

@@ -1013,6 +1013,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
 // Per-slot search workspace (visited bitmaps, clear lists, queue counters, the lean kernel's push log)
 // for a full-occupancy grid, allocated once at index load so that no search pays for it (at C5 the
 // bitmaps alone are 32 GB). Searches that need more (other LUT sizes, larger logs) still grow it.
+// The inline-row lean kernel's tagged visited words for `slots` slots (zeroed: generation 0 is never a query's)
+static void ensure_tagged(DeviceIndex &ix, int slots)
+{
+    const int64_t words = ((ix.ntotal + 15) / 16 + 3) / 4 * 4;
+    if (ix.vis_tag && ix.tag_slots >= slots && ix.tag_words == words)
+        return;
+    if (ix.vis_tag)
+        DRM_HIP_CHECK(hipFree(ix.vis_tag));
+    if (ix.vis_gen)
+        DRM_HIP_CHECK(hipFree(ix.vis_gen));
+    ix.vis_tag = nullptr;
+    ix.vis_gen = nullptr;
+    DRM_HIP_CHECK(malloc_big((void **)&ix.vis_tag, sizeof(uint32_t) * (size_t)slots * (size_t)words, kBigVisited));
+    DRM_HIP_CHECK(hipMemset(ix.vis_tag, 0, sizeof(uint32_t) * (size_t)slots * (size_t)words));
+    DRM_HIP_CHECK(hipMalloc(&ix.vis_gen, sizeof(uint32_t) * (size_t)slots));
+    DRM_HIP_CHECK(hipMemset(ix.vis_gen, 0, sizeof(uint32_t) * (size_t)slots));
+    ix.tag_slots = slots;
+    ix.tag_words = words;
+}
+
 void reserve_search_scratch(DeviceIndex &ix)
 {
     int cus = 0;
@@ -1022,14 +1042,20 @@ void reserve_search_scratch(DeviceIndex &ix)
         return;
     const int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     const int slots = cus * per_cu;
-    ix.vis_words = std::max<int64_t>((ix.ntotal + 31) / 32, 1);
-    ix.clear_cap = 16384;
-    DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words, kBigVisited));
-    DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
-    DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)slots * (size_t)ix.clear_cap));
-    ix.n_slots = slots;
+    if (ix.rows) { // the inline-row kernel's tagged words; the plain bitmap waits for a search that needs it
+        ensure_tagged(ix, slots);
+    } else {
+        ix.vis_words = std::max<int64_t>((ix.ntotal + 31) / 32, 1);
+        ix.clear_cap = 16384;
+        DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words, kBigVisited));
+        DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
+        DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)slots * (size_t)ix.clear_cap));
+        ix.n_slots = slots;
+    }
     DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
     const int cap = std::max(ix.log_cap_req, 128 + 64); // what the lean kernel asks for at ef = 128
+    if (ix.log)
+        DRM_HIP_CHECK(hipFree(ix.log));
     DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)slots * (size_t)cap));
     ix.log_cap = cap;
     ix.log_slots = slots;
@@ -1071,9 +1097,13 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
     int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
-    // (re)allocate per-slot workspace
+    // (re)allocate per-slot workspace: the inline-row lean kernel uses the tagged words, the others the bitmap
+    const bool fast_path = ix.use_fast && !ix.try_sorted && hnsw_pq_fast_supported(ix, k, efc);
+    const bool tagged = fast_path && ix.rows != nullptr;
     const int64_t words = (ix.ntotal + 31) / 32;
-    if (slots > ix.n_slots || words != ix.vis_words) {
+    if (tagged)
+        ensure_tagged(ix, std::max(slots, ix.tag_slots));
+    else if (slots > ix.n_slots || words != ix.vis_words) {
         if (ix.visited)
             DRM_HIP_CHECK(hipFree(ix.visited));
         if (ix.clear_list)
@@ -1130,16 +1160,24 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.x_aligned16 = ((uintptr_t)d_x % 16) == 0;
 
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
-    if (ix.use_fast && !ix.try_sorted && hnsw_pq_fast_supported(ix, k, efc)) {
+    if (fast_path) {
         // the lean kernel (hnsw_pq_fast.hip); k == ef logs accepted pushes per slot
         const int cap = std::max(ix.log_cap_req, efc + 64); // one hop appends <= 64 after a compaction
-        if (!ix.log || ix.log_cap != cap || ix.log_slots < ix.n_slots) {
+        const int need = std::max(tagged ? ix.tag_slots : ix.n_slots, slots);
+        if (!ix.log || ix.log_cap != cap || ix.log_slots < need) {
             if (ix.log)
                 DRM_HIP_CHECK(hipFree(ix.log));
             ix.log = nullptr;
-            DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)ix.n_slots * (size_t)cap));
+            DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)need * (size_t)cap));
             ix.log_cap = cap;
-            ix.log_slots = ix.n_slots;
+            ix.log_slots = need;
+        }
+        if (tagged) {
+            a.visited = ix.vis_tag;
+            a.vis_words = ix.tag_words;
+            a.vis_gen = ix.vis_gen;
+            a.clear_list = nullptr;
+            a.clear_cap = 0;
         }
         a.log = ix.log;
         a.log_cap = ix.log_cap;

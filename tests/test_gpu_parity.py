@@ -152,6 +152,40 @@ def test_search_syn20k_bitexact(syn20k):
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
 
 
+def test_search_visited_generation_wrap(syn20k):
+    """The inline-row lean kernel tags each visited word with the query's 16-bit generation instead of clearing
+    its bits after every query. Generations set just below the wrap, and a small grid (256 slots, ~8 queries
+    each), make every slot restart its words mid-batch: results stay bit-identical to the oracle, across
+    repeated launches on one handle and across K = 128 / K = 5 (both variants share the generations). The hook
+    restarts the words at the generation it sets (generations only ever increase between wraps)."""
+    import ctypes as C
+    from deepreadmapper_amd import read_index
+    from deepreadmapper_amd._native import check, lib
+    w, fx = syn20k["w"], syn20k["fx"]
+    q = w.q_emb
+    L = lib()
+    L.drm_debug_search_generation.argtypes = [C.c_void_p, C.c_uint32]
+    ix = read_index(syn20k["index"])
+    check(L.drm_index_set_search_waves(ix.handle, 1))
+    Do, Io, nd, nh = O.hnswpq_search(fx, q, 128, 128)
+    D5o, I5o, nd5, nh5 = O.hnswpq_search(fx, q, 5, 128)
+    for gen in (0xFFFD, 0xFFFF, 7):
+        check(L.drm_debug_search_generation(ix.handle, gen))
+        for _ in range(2):
+            D, I, st = ix.search(q, 128, 128)
+            bad = np.flatnonzero((I != Io).any(axis=1))
+            assert bad.size == 0, f"generation {gen:#x}: {bad.size} rows differ, first {bad[:8]}"
+            assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))
+            assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+            D5, I5, st5 = ix.search(q, 5, 128)
+            assert np.array_equal(I5, I5o) and np.array_equal(D5.view(np.uint32), D5o.view(np.uint32)), f"{gen:#x}"
+            assert st5.ndis == int(nd5.sum()) and st5.nhops == int(nh5.sum())
+    check(L.drm_index_set_search_waves(ix.handle, 0))
+    D, I, st = ix.search(q, 128, 128)
+    assert np.array_equal(I, Io) and st.ndis == int(nd.sum())
+    ix.free()
+
+
 def test_search_syn20k_sorted_pass(syn20k, monkeypatch):
     """The opt-in sorted-array pass + exact fallback equals the oracle on the dense index."""
     monkeypatch.setenv("DRM_SEARCH_SORTED", "1")

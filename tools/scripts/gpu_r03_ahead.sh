@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: parity of a search-kernel variant library (DRM_LIB), then a same-box A/B at C5 against the baseline
-# build, section stamps of the variant, and the visited-bitmap locality probe.
+# build, and section stamps of both (FIX128 stamped build).
 # Usage: bash tools/scripts/gpu_r03_ahead.sh ab/base.so ab/variant.so
 BASE=$1; VAR=$2
 set -o pipefail
@@ -10,7 +10,4 @@ DRM_LIB=$PWD/$VAR timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py
 tail -1 gpurun_out/ahead_tests.log
 for r in 1 2; do for lib in $BASE $VAR; do echo "== $lib"; DRM_LIB=$PWD/$lib timeout -k 10 600 python -u tools/scripts/search_c5.py 2>&1 | grep "^search" || exit 1; done; done
 for lib in $BASE $VAR; do echo "== $lib K=5"; DRM_LIB=$PWD/$lib timeout -k 10 600 python -u tools/scripts/search_c5.py --k 5 2>&1 | grep "^search" || exit 1; done
-DRM_LIB=$PWD/$VAR DRM_SEARCH_STAMPS=1 timeout -k 10 600 python -u tools/scripts/stamps.py c5gru > gpurun_out/ahead_stamps.txt 2>&1 || { tail -5 gpurun_out/ahead_stamps.txt; exit 1; }
-cat gpurun_out/ahead_stamps.txt
-timeout -k 10 600 python -u tools/scripts/vis_locality.py > gpurun_out/vis_locality.txt 2>&1 || { tail -5 gpurun_out/vis_locality.txt; exit 1; }
-cat gpurun_out/vis_locality.txt
+for lib in $BASE $VAR; do echo "== stamps $lib"; DRM_LIB=$PWD/$lib DRM_SEARCH_STAMPS=1 timeout -k 10 600 python -u tools/scripts/stamps.py c5gru 2>&1 | grep -v "^\[bench\]" || exit 1; done

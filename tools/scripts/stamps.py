@@ -44,7 +44,9 @@ if os.environ.get("DRM_SEARCH_FAST", "1") != "0":
     print(f"row prediction hits {int(out[8])} of {int(out[9])} hops ({out[8] / max(out[9], 1) * 100:.1f} %)")
     if out[10]:
         print(f"two-ahead hits (row, distances and visited words prepared) {int(out[10])} ({out[10] / max(out[9], 1) * 100:.1f} %)")
-    out[8] = out[9] = out[10] = 0
+    if out[11]:
+        print(f"full-heap replace pushes {int(out[11])} ({out[11] / max(out[9], 1):.2f} per hop)")
+    out[8] = out[9] = out[10] = out[11] = 0
 tot = float(out.sum())
 for n, v in zip(names, out):
     print(f"{n:32s} {v / tot * 100:6.2f} %")
