@@ -60,9 +60,10 @@ struct DeviceIndex {
     float *centroids = nullptr;    // [M][ksub][dsub] f32
     uint8_t *codes = nullptr;      // [ntotal][code_size]
     int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
-    // lean kernel's level-0 rows with the neighbours' PQ codes inline: node i's row is deg0 ids (int32) then
-    // deg0 8-byte codes, row_words int32 per row (384 B at M_hnsw = 16), so one row fetch brings the codes the
-    // hop's distances need; null when the index shape has no such layout (PQ != 8 x 8)
+    // lean kernel's level-0 rows with the neighbours' PQ codes inline: node i's row is, per link, its id (int32) and
+    // its 8-byte code (12 B per link), row_words int32 per row (384 B at M_hnsw = 16), so one dwordx3 load brings a
+    // hop its links and the codes its distances need; null when the index shape has no such
+    // layout (PQ != 8 x 8)
     int32_t *rows = nullptr;
     int32_t row_words = 0;
     uint2 *upper_codes = nullptr;  // the code of every upper_nbr entry (0 for -1): greedy hops fetch ids + codes together

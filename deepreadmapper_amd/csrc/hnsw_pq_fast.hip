@@ -440,6 +440,31 @@ __device__ __forceinline__ void sort128(uint64_t &x0, uint64_t &x1, int lane)
     }
 }
 
+// Link `lane` of an inline level-0 row (DeviceIndex::rows): its id and its 8-byte PQ code, interleaved as 12 bytes
+// per link, so the whole row (32 links = 384 B at M_hnsw = 16) is one dwordx3 load of the wave instead of an id load
+// and a code load: every VMEM instruction a hop issues costs the CU's memory pipeline the same ~80-150 cycles
+// whatever the footprint (tools/microbench/vispattern.hip). Lanes past deg0 get (-1, 0).
+__device__ __forceinline__ void load_link(const int32_t *row, int lane, int deg0, int32_t &id, uint2 &code)
+{
+    id = -1;
+    code = make_uint2(0u, 0u);
+    if (lane < deg0) {
+        const int32_t *e = row + 3 * lane;
+        id = e[0];
+        code = make_uint2((uint32_t)e[1], (uint32_t)e[2]);
+    }
+}
+
+// The raw 12 bytes of link j of an inline row, loaded by every lane (lanes past deg0 read link 0 and are masked at
+// the use): no branch around the load, so the compiler can count it and leave it in flight (DRM_PQ_ASYNC).
+struct __attribute__((aligned(4))) Link3 {
+    uint32_t x, y, z;
+};
+__device__ __forceinline__ Link3 load_link_raw(const int32_t *row, int lane, int deg0)
+{
+    return *reinterpret_cast<const Link3 *>(row + 3 * (lane < deg0 ? lane : 0));
+}
+
 // greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss], the inline
 // layout's form of greedy_upper (pq_common.h): a hop loads its upper-level list and the links' codes together
 // (SearchArgs::upper_codes), one memory round trip per hop instead of two. Same distances, same order.
@@ -546,6 +571,19 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
 
 #ifndef DRM_PQ_VIS_LOAD
 #define DRM_PQ_VIS_LOAD 1 // inline kernel: visited test by an L2 load, fresh links marked afterwards (0: test-and-set)
+#endif
+
+#ifndef DRM_PQ_LOGSTAGE
+// k == ef: accepted pushes are staged in a 64-entry register buffer (lane sn takes the push loop's scalars) and stored to the slot's log 64 at a time, instead of one store instruction per hop (0: per-hop store)
+#define DRM_PQ_LOGSTAGE 1
+#endif
+
+#ifndef DRM_PQ_ASYNC
+// inline kernel: the predicted next row is loaded by an unconditional instruction and only waited for at the next
+// hop, and the visited test is an unconditional load, so a hop waits for its visited answer alone (vmcnt counts the
+// row load still in flight). 0: the row load sits in a branch, and the compiler waited for it right away (the copy
+// into the loop-carried registers), i.e. after the ADC and the prediction, on the hop's critical path.
+#define DRM_PQ_ASYNC 1
 #endif
 
 #ifndef DRM_PQ_SPEC
@@ -655,6 +693,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             rv = lane > pos ? sh : (lane == pos ? v : rv);
             thr = (uint32_t)__builtin_amdgcn_readlane((int)hi32(rv), k - 1);
         };
+        // DRM_PQ_LOGSTAGE: accepted pushes not yet stored, lanes [0, sn) of (sbh, sbl) = (key, id ^ 2^31) in log order
+        uint32_t sbh = 0u, sbl = 0u;
+        int sn = 0;
+        // compacts the stored log to the current k results when the staged entries would overflow it (T = the heap
+        // root's key: the k-th smallest of every accepted push so far, stored or staged, so no entry of the final
+        // result set is dropped), then appends the staged entries
+        auto log_flush = [&]() {
+            if (logn + sn > a.log_cap) {
+                const uint32_t T = hi32(root);
+                const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
+                logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
+                    __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }, lane);
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            if (lane < sn)
+                __hip_atomic_store(lg + logn + lane, ((uint64_t)sbh << 32) | sbl, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            logn += sn;
+            sn = 0;
+        };
         if (LOGRES) {
             if (lane == 0)
                 lg[0] = root;
@@ -685,6 +744,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // INL: a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row
         // prediction can skip links back to nodes already expanded before the visited test has answered
         uint32_t popped_bits = 0u;
+        Link3 praw{0xFFFFFFFFu, 0u, 0u}; // DRM_PQ_ASYNC: the predicted row's link `lane`, raw (pred = -1: none yet)
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
         while (nvalid > 0) {
             // pop_min: smallest key among valid slots, ties -> the highest slot
@@ -733,11 +793,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const uint32_t h0 = pop_hash(v0);
                 if (lane == (int)((h0 >> 5) & 63u))
                     popped_bits |= 1u << (h0 & 31u);
-                if (!hit) {
-                    const int32_t *row = a.rows + (size_t)v0 * (size_t)a.row_words;
-                    v1 = lane < deg0 ? row[lane] : -1;
-                    c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(row + deg0)[lane] : make_uint2(0u, 0u);
-                }
+                if (DRM_PQ_ASYNC) {
+                    if (!hit)
+                        praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
+                    v1 = lane < deg0 ? (int32_t)praw.x : -1;
+                    c8_pref = lane < deg0 ? make_uint2(praw.y, praw.z) : make_uint2(0u, 0u);
+                } else if (!hit)
+                    load_link(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0, v1, c8_pref);
             } else if (!hit)
                 v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
             const uint64_t negm = ballot(v1 < 0) & deg0m;
@@ -755,7 +817,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 // own earlier marks are at L2, never in its L1), and only the fresh links are marked afterwards.
                 // Exact: this wave alone writes its words, its earlier marks were issued before this load, and a
                 // repeated id in one row is fresh once (check_dups below) and so marked once.
-                if (act)
+                if (DRM_PQ_ASYNC) // every lane loads (the inactive ones word 0), no branch
+                    old = __hip_atomic_load(&vis[act ? (v1 >> 4) : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (act)
                     old = __hip_atomic_load(&vis[v1 >> 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (use_spec) {
                 c8 = c8_pref;
@@ -781,11 +845,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const int32_t mid = dp == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
                 const uint32_t mm = wave_min_u32(mk);
                 pred = -1;
-                if (mm != 0xFFFFFFFFu) {
+                if (DRM_PQ_ASYNC) {
+                    // no prediction (the heap and the row hold nothing valid): load v0's row again, pred stays -1
+                    int32_t pnode = v0;
+                    if (mm != 0xFFFFFFFFu) {
+                        pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
+                        pnode = pred;
+                    }
+                    praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
+                } else if (mm != 0xFFFFFFFFu) {
                     pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
-                    const int32_t *prow = a.rows + (size_t)pred * (size_t)a.row_words;
-                    v1_pref = lane < deg0 ? prow[lane] : -1;
-                    c8_pref = lane < deg0 ? reinterpret_cast<const uint2 *>(prow + deg0)[lane] : make_uint2(0u, 0u);
+                    load_link(a.rows + (size_t)pred * (size_t)a.row_words, lane, deg0, v1_pref, c8_pref);
                 }
             }
             // visited in this query: (tagged) the word carries this query's generation and the node's bit
@@ -874,7 +944,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (key < thr)
                         add_result(pack(key, __builtin_amdgcn_readlane(v1, l)));
                 }
-                const uint64_t val = pack(key, __builtin_amdgcn_readlane(v1, l));
+                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                const uint64_t val = pack(key, idl);
                 if (kc == ef) { // MinimaxHeap::push on a full heap: pop the max, push val
                     if (key >= hi32(root))
                         continue;
@@ -909,10 +980,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 }
                 ++nvalid;
                 accm |= 1ull << l;
+                if (LOGRES && DRM_PQ_LOGSTAGE) {
+                    if (sn == 64)
+                        log_flush();
+                    const bool at = lane == sn; // lane sn takes the entry (one compare, two selects)
+                    sbh = at ? key : sbh;
+                    sbl = at ? lo32(val) : sbl;
+                    ++sn;
+                }
             }
             if (DRM_PQ_SROOT && replaced && lane == 63)
                 hp.R = root;
-            if (LOGRES && accm) {
+            if (LOGRES && !DRM_PQ_LOGSTAGE && accm) {
                 const int na = __builtin_popcountll(accm);
                 if (logn + na > a.log_cap) {
                     // compact in place: the current result set (k entries) replaces the log
@@ -945,6 +1024,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 
         // --- SingleResultHandler::end (heap_reorder): ascending (distance, id), (+inf, -1) padding
         if (LOGRES) {
+            if (DRM_PQ_LOGSTAGE && sn)
+                log_flush();
             __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
             __syncthreads();
             const uint32_t T = kc == ef ? hi32(root) : 0xFFFFFFFFu;
@@ -1002,8 +1083,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 
-// DeviceIndex::rows: row i = nbr0[i][0 .. deg0) then, for each link, its 8-byte code (0 past the row's end).
-// One wave per node; lane j < deg0 writes link j's id and code.
+// DeviceIndex::rows: row i holds, for each link j < deg0, its id then its 8-byte code at words [3j, 3j + 3) (code 0
+// past the row's end). One wave per node; lane j < deg0 writes link j.
 __global__ __launch_bounds__(256) void build_inline_rows_kernel(const int32_t *nbr0, const uint8_t *codes, int64_t n,
                                                                 int deg0, int row_words, int32_t *rows)
 {
@@ -1012,10 +1093,11 @@ __global__ __launch_bounds__(256) void build_inline_rows_kernel(const int32_t *n
     if (i >= n || j >= deg0)
         return;
     const int32_t v = nbr0[i * deg0 + j];
-    int32_t *row = rows + i * (int64_t)row_words;
-    row[j] = v;
-    reinterpret_cast<uint2 *>(row + deg0)[j] = v >= 0 ? *reinterpret_cast<const uint2 *>(codes + (size_t)v * 8)
-                                                      : make_uint2(0u, 0u);
+    int32_t *e = rows + i * (int64_t)row_words + 3 * j;
+    const uint2 c = v >= 0 ? *reinterpret_cast<const uint2 *>(codes + (size_t)v * 8) : make_uint2(0u, 0u);
+    e[0] = v;
+    e[1] = (int32_t)c.x;
+    e[2] = (int32_t)c.y;
 }
 
 __global__ __launch_bounds__(256) void build_upper_codes_kernel(const int32_t *upper_nbr, const uint8_t *codes, int64_t n,
@@ -1035,7 +1117,7 @@ void build_inline_rows(DeviceIndex &ix)
     if (ix.pq_M != 8 || ix.pq_nbits != 8 || ix.code_size != 8 || ix.deg0 > 64 || ix.deg0 < 1 || ix.vmode != 0 ||
         ix.ntotal <= 0)
         return;
-    const int64_t words = ((int64_t)ix.deg0 * 3 + 31) / 32 * 32; // deg0 ids + 2 deg0 code words, 128-B rows
+    const int64_t words = ((int64_t)ix.deg0 * 3 + 31) / 32 * 32; // deg0 x (id, 2 code words), 128-B rows
     DRM_HIP_CHECK(malloc_big((void **)&ix.rows, sizeof(int32_t) * (size_t)ix.ntotal * (size_t)words, kBigIndex));
     ix.row_words = (int32_t)words;
     ix.device_bytes += (int64_t)sizeof(int32_t) * ix.ntotal * words;
