@@ -367,6 +367,112 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 #define DRM_SW_ROWS2 1 // two DP rows in flight per pass (sw_row2_f16); 0: one row at a time (sw_row_f16)
 #endif
 
+#ifndef DRM_SW_INT
+// 1: scores as 16-bit integers (two per register), the diagonal add as one 32-bit add over both halves, the
+// three-way max as v_pk_maximum3_f16 on the integer bit patterns, the -1 floored at 0 as a saturating packed
+// subtract (sw_row_i16 / sw_row2_i16); 0: fp16 multiples of 2^-10 (sw_row_f16 / sw_row2_f16)
+#define DRM_SW_INT 1
+#endif
+
+// ---- integer cells (DRM_SW_INT). A score s (0 <= s <= 1023) is the 16-bit pattern s, i.e. the fp16 subnormal
+// s * 2^-24: fp16 ordering of non-negative patterns below 0x7C00 is the integer ordering (subnormals included:
+// fp16 denormals are kept, the default FP mode), so v_pk_maximum3_f16 is an exact integer max3. The diagonal
+// term (+2 on a match) is added by v_add_u32 across both halves: the low half stays below 2^16 (s <= 1023 + 2),
+// so no carry crosses. One cell pair costs a 32-bit add (2 cycles per wave64 instruction on gfx950) instead of a
+// packed add (4 cycles), profiles/r02/valu_rate_probe.txt: 12 instead of 14 issue cycles per cell pair.
+__device__ __forceinline__ uint32_t imax3(uint32_t a, uint32_t b, uint32_t c)
+{
+    const h2 r = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b)),
+                                               __builtin_bit_cast(h2, c));
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t idec(uint32_t a) // max(0, s - 1) in both halves: v_pk_sub_u16 ... clamp
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a), (u16x2){1, 1}));
+}
+
+template <int LQ>
+__device__ __forceinline__ void sw_row_i16(uint32_t (&H)[LQ], const uint32_t *pp, uint32_t &best)
+{
+    uint4 P = *reinterpret_cast<const uint4 *>(pp);
+    uint32_t td = P.x; // column 0: the diagonal is the zero border
+    uint32_t left = 0u;
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+        const uint32_t up = H[j];
+        uint32_t tn = 0u;
+        if (j + 1 < LQ) {
+            const int n = j + 1;
+            if ((n & 3) == 0)
+                P = *reinterpret_cast<const uint4 *>(pp + n);
+            tn = up + ((n & 3) == 0 ? P.x : (n & 3) == 1 ? P.y : (n & 3) == 2 ? P.z : P.w);
+        }
+        const uint32_t h = idec(imax3(td, up, left));
+        H[j] = h;
+        left = h;
+        best = imax3(best, h, h);
+        td = tn;
+    }
+}
+
+// sw_row2_f16's two-rows-in-flight schedule on integer cells
+template <int LQ, int PF = 2>
+__device__ __forceinline__ void sw_row2_i16(uint32_t (&H)[LQ], const uint32_t *pa, const uint32_t *pb, uint32_t &best)
+{
+    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
+    uint4 A[NS], B[NS];
+#pragma unroll
+    for (int g = 0; g < NS; ++g)
+        if (g < NG) {
+            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
+            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
+        }
+    auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
+    uint32_t tda = A[0].x, tdb = B[0].x; // column 0: zero-border diagonal
+    uint32_t lefta = 0u, leftb = 0u;
+#pragma clang loop unroll(full)
+    for (int j = 0; j <= LQ; ++j) {
+        if ((j & 3) == 0 && j >= 4) {
+            const int gd = (j >> 2) - 1, gn = gd + NS;
+            if (gn < NG) {
+                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
+                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t ha = 0u, hb = 0u;
+        if (j < LQ) {
+            const uint32_t up = H[j];
+            uint32_t tn = 0u;
+            if (j + 1 < LQ) {
+                const int n = j + 1;
+                tn = up + word(A[(n >> 2) % NS], n & 3);
+            }
+            const uint32_t h = idec(imax3(tda, up, lefta));
+            H[j] = h;
+            lefta = h;
+            tda = tn;
+            ha = h;
+        }
+        if (j >= 1) {
+            const int c = j - 1;
+            const uint32_t up = H[c];
+            uint32_t tn = 0u;
+            if (c + 1 < LQ) {
+                const int n = c + 1;
+                tn = up + word(B[(n >> 2) % NS], n & 3);
+            }
+            const uint32_t h = idec(imax3(tdb, up, leftb));
+            H[c] = h;
+            leftb = h;
+            tdb = tn;
+            hb = h;
+        }
+        best = imax3(best, ha, hb);
+    }
+}
+
 __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
 {
     const int k = (c >> 1) & 3; // A=0x41 -> 0, C=0x43 -> 1, T=0x54 -> 2, G=0x47 -> 3
@@ -533,7 +639,9 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             uint32_t word = 0;
             if (kb < 5 && j < qlen && j < LQ) {
                 const int c = qbuf[j];
-                word = (c == acgt_byte(ka) ? 0x1800u : 0u) | (c == acgt_byte(kb) ? 0x18000000u : 0u);
+                // the diagonal term: +2 on a match (the -1 every cell takes makes it +1), 2^-9 in the fp16 form
+                const uint32_t t = DRM_SW_INT ? 0x0002u : 0x1800u;
+                word = (c == acgt_byte(ka) ? t : 0u) | (c == acgt_byte(kb) ? t << 16 : 0u);
             }
             pprof[e] = word;
         }
@@ -544,11 +652,19 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         for (int c0 = tid; c0 < ncand; c0 += 128) {
             const int c1 = c0 + 64;
             const bool has_b = c1 < ncand;
+#if DRM_SW_INT
+            uint32_t H[LQ];
+#pragma unroll
+            for (int j = 0; j < LQ; ++j)
+                H[j] = 0u;
+            uint32_t best = 0u;
+#else
             h2 H[LQ];
 #pragma unroll
             for (int j = 0; j < LQ; ++j)
                 H[j] = (h2){(_Float16)0.0f, (_Float16)0.0f};
             h2 best = {(_Float16)0.0f, (_Float16)0.0f};
+#endif
             const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
             // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
             // block in flight while the current one is consumed), not one byte load per row
@@ -610,17 +726,31 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             for (; i + 1 < L; i += 2) {
                 const uint32_t *p0 = row(i);
                 const uint32_t *p1 = row(i + 1);
+#if DRM_SW_INT
+                sw_row2_i16<LQ>(H, p0, p1, best);
+#else
                 sw_row2_f16<LQ>(H, p0, p1, best);
+#endif
             }
 #endif
-            for (; i < L; ++i)
+            for (; i < L; ++i) {
+#if DRM_SW_INT
+                sw_row_i16<LQ>(H, row(i), best);
+#else
                 sw_row_f16<LQ>(H, row(i), best);
+#endif
+            }
+#if DRM_SW_INT
+            const int score_a = (int)(best & 0xFFFFu), score_b = (int)(best >> 16);
+#else
+            const int score_a = (int)((float)best.x * 1024.0f), score_b = (int)((float)best.y * 1024.0f);
+#endif
             const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
             a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
-            a.cand_scores[q * a.cmax + c0] = (int32_t)((float)best.x * 1024.0f);
+            a.cand_scores[q * a.cmax + c0] = score_a;
             if (has_b) {
                 a.cand_ids[q * a.cmax + c1] = dense_dyn ? (uint64_t)nb[c1] : wb;
-                a.cand_scores[q * a.cmax + c1] = (int32_t)((float)best.y * 1024.0f);
+                a.cand_scores[q * a.cmax + c1] = score_b;
             }
         }
         if (__ballot(flagged) != 0ull && lane == 0)
