@@ -38,7 +38,9 @@ SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, true>"  # what C3/C4/C5 
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<152>"
 SW_VALU_PER_CELL_PAIR = 1067 / 304  # static ISA count of sw_score_f16_kernel<152>'s two-row block: 1067 VALU per 2 x 152 cell pairs
-SW_PACKED_ISSUE_CYC = 4.0  # cycles per wave64 packed-f16 VALU instruction per SIMD (profiles/r02/valu_rate_probe.txt)
+# its mix (integer cells, DRM_SW_INT): 761 packed 16-bit (v_pk_maximum3_f16, v_pk_sub_u16) at 4 cycles per wave64
+# instruction per SIMD and 306 32-bit (v_add_u32, ...) at 2 (profiles/r02/valu_rate_probe.txt): average issue cycles
+SW_ISSUE_CYC_PER_VALU = (761 * 4.0 + 306 * 2.0) / 1067
 
 
 def cpu_model():
@@ -692,16 +694,17 @@ def main():
     sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, pkey)
     ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
     sw_gcups = cells / (sw_ms * 1e-3) / 1e9
-    # SW roofline = the hardware's VALU issue rate: 4 SIMDs per CU, one packed-f16 wave64 instruction per SIMD every
-    # SW_PACKED_ISSUE_CYC cycles. Instructions per launch: the committed PMC count of this workload's SW kernel when
-    # there is one (SQ_INSTS_VALU per dispatch, scaled to this run's cells), else the static DP count (one wave
-    # instruction advances 64 lanes x 2 candidates by one cell; 3.51 per cell pair)
-    sw_peak_instr = ncu * 4 * CLOCK_HZ / SW_PACKED_ISSUE_CYC
+    # SW roofline = the hardware's VALU issue rate: 4 SIMDs per CU, each issuing one wave64 VALU instruction per 4
+    # cycles (packed 16-bit) or per 2 cycles (32-bit). Instructions per launch: the committed PMC count of this
+    # workload's SW kernel when there is one (SQ_INSTS_VALU per dispatch), else the static DP count (one wave
+    # instruction advances 64 lanes x 2 candidates by one cell; 3.51 per cell pair); issue cycles = instructions x
+    # the DP block's average cycles per instruction (SW_ISSUE_CYC_PER_VALU)
+    sw_peak_cyc = ncu * 4 * CLOCK_HZ
     sw_instr_static = cells / 128.0 * SW_VALU_PER_CELL_PAIR
     sw_instr, sw_instr_src = sw_instr_static, "static ISA count of the DP block"
     if sw_pmc and "SQ_INSTS_VALU" in sw_pmc and (Q, K) == (1_250_000, 128):
         sw_instr, sw_instr_src = float(sw_pmc["SQ_INSTS_VALU"]), f"{sw_prof_path}: SQ_INSTS_VALU per dispatch"
-    sw_achieved_instr = sw_instr / (sw_ms * 1e-3)
+    sw_achieved_cyc = sw_instr * SW_ISSUE_CYC_PER_VALU / (sw_ms * 1e-3)
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
@@ -728,7 +731,7 @@ def main():
             "vs_baseline": None,
             "dtype": ("fp32 (L2 distances)" if flat else "fp32 (PQ-ADC distances)") + (
                 " + int32 (SW DP, bit-profile u16 kernel)" if os.environ.get("DRM_SW_BITPROFILE") == "1" else
-                " + fp16 fixed-point SW DP (2^-10 units, exact for scores < 1024)"),
+                " + u16 integer SW DP (two cells per register)"),
             "data": f"synthetic (seeded genome/reads, {EMBED_DESC[args.embed]} embeddings; no network)",
             "config": {"workload": workload, "n_refs": int(len(refs)), "queries_per_gpu": Q, "ef": EF, "k": K,
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
@@ -746,13 +749,15 @@ def main():
                          "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
                          if pmc and "valu_issue_frac" in pmc else None,
                          "issue": issue_ceiling(pmc, float(nhops.sum()), search_ms)},
-            "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_achieved_instr / 1e9, 2),
-                            "peak": round(sw_peak_instr / 1e9, 2), "unit": "G wave-instr/s (packed f16 VALU issue)",
-                            "frac": round(sw_achieved_instr / sw_peak_instr, 4), "instr_per_launch": sw_instr,
+            "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_achieved_cyc / 1e9, 2),
+                            "peak": round(sw_peak_cyc / 1e9, 2), "unit": "G SIMD VALU-issue cycles/s",
+                            "frac": round(sw_achieved_cyc / sw_peak_cyc, 4), "instr_per_launch": sw_instr,
                             "instr_source": sw_instr_src, "gcups": round(sw_gcups, 1),
                             "valu_per_cell_pair": round(SW_VALU_PER_CELL_PAIR, 3),
-                            "note": "frac = VALU issue slots used / the SIMDs' packed-issue capacity (4 SIMDs x 2.4 GHz / "
-                                    "4 cycles per CU); the DP's op count per cell pair is reported separately"},
+                            "issue_cycles_per_cell_pair": round(SW_VALU_PER_CELL_PAIR * SW_ISSUE_CYC_PER_VALU, 2),
+                            "note": "frac = VALU issue cycles used (packed 16-bit 4, 32-bit 2 cycles per wave64 "
+                                    "instruction) / the SIMDs' capacity (1,024 SIMDs x 2.4 GHz); the DP's op count per "
+                                    "cell pair is reported separately"},
             "cpu_baseline": cpu,
             "gather": gather,
             "host_path": host,
