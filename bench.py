@@ -36,11 +36,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
 SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, true>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline codes) launch (hnsw_pq_fast.hip)
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
-SW_KERNEL = "sw_score_f16_kernel<152>"
-SW_VALU_PER_CELL_PAIR = 1067 / 304  # static ISA count of sw_score_f16_kernel<152>'s two-row block: 1067 VALU per 2 x 152 cell pairs
-# its mix (integer cells, DRM_SW_INT): 761 packed 16-bit (v_pk_maximum3_f16, v_pk_sub_u16) at 4 cycles per wave64
-# instruction per SIMD and 306 32-bit (v_add_u32, ...) at 2 (profiles/r02/valu_rate_probe.txt): average issue cycles
-SW_ISSUE_CYC_PER_VALU = (761 * 4.0 + 306 * 2.0) / 1067
+SW_KERNEL = "sw_score_f16_kernel<150>"  # 150 DP columns: a tagged 150 bp read without its "<" / ">" ends
+SW_VALU_PER_CELL_PAIR = 1053 / 300  # static ISA count of sw_score_f16_kernel<150>'s two-row block: 1053 VALU per 2 x 150 cell pairs
+# its mix (integer cells, DRM_SW_INT): 751 packed 16-bit (v_pk_maximum3_f16, v_pk_sub_u16) at 4 cycles per wave64
+# instruction per SIMD and 302 32-bit (v_add_u32, ...) at 2 (profiles/r02/valu_rate_probe.txt): average issue cycles
+SW_ISSUE_CYC_PER_VALU = (751 * 4.0 + 302 * 2.0) / 1053
 
 
 def cpu_model():
@@ -700,7 +700,9 @@ def main():
     # instruction advances 64 lanes x 2 candidates by one cell; 3.51 per cell pair); issue cycles = instructions x
     # the DP block's average cycles per instruction (SW_ISSUE_CYC_PER_VALU)
     sw_peak_cyc = ncu * 4 * CLOCK_HZ
-    sw_instr_static = cells / 128.0 * SW_VALU_PER_CELL_PAIR
+    # the DP's own cells: the tags of the 152-byte queries are not DP columns (sw_rerank.hip)
+    dp_cells = float(Q) * K * refs.shape[1] * max(queries.shape[1] - 2, 1)
+    sw_instr_static = dp_cells / 128.0 * SW_VALU_PER_CELL_PAIR
     sw_instr, sw_instr_src = sw_instr_static, "static ISA count of the DP block"
     if sw_pmc and "SQ_INSTS_VALU" in sw_pmc and (Q, K) == (1_250_000, 128):
         sw_instr, sw_instr_src = float(sw_pmc["SQ_INSTS_VALU"]), f"{sw_prof_path}: SQ_INSTS_VALU per dispatch"

@@ -126,6 +126,10 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 #define DRM_PQ_TAGMARK 1
 #endif
 
+#ifndef DRM_PQ_REPL1
+#define DRM_PQ_REPL1 1 // full-heap replace as one routine with one cross-lane round trip (Heap::replace128)
+#endif
+
 #ifndef DRM_PQ_SROOT
 // ef = 128 replace pushes keep the root (slot 0) in scalar registers only; lane 63's R is refreshed once per hop
 #define DRM_PQ_SROOT 1
@@ -341,6 +345,55 @@ struct Heap {
             return val;
         }
         L = in_mask(1ull << ((1u << (6 - h)) - 1u)) ? val : L; // the chain slot at index h
+        return rootv;
+    }
+
+    // pop128v2 then push128v2(vnew) with both cross-lane fetches issued together from the pre-pop registers
+    // (DRM_PQ_REPL1): one ds_bpermute round trip per full-heap replace instead of two in sequence.
+    //  * pop: lane p on the path writes its chosen child slot with that child's own chosen child (chv of lane ch_p),
+    //    or with slot 127's value when p is the path's last node; the fetch from lane ch_p needs no path knowledge,
+    //    so it leaves at once and the path (ballots, scalar masks) is formed while it is in flight;
+    //  * push: chain holder c (lanes 1, 3, 7, 15, 31, 63; slot 2c + 1 in its L) takes its father, slot c, held in
+    //    lane c >> 1's L. After the pop, slot c holds lane c's own chv (or slot 127's value) if lane c >> 1 is on the
+    //    path and took its L child, else its pre-pop value: the only cross-lane part is the pre-pop fetch.
+    // Same slots, same values as pop128v2 + push128v2; returns the root after the push.
+    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, const PathConst &pc, int lane)
+    {
+        const uint64_t val = readlane64(L, 63);            // slot 127
+        const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child
+        const bool takeL = in_mask(lm);
+        const uint64_t chv = takeL ? L : R;
+        const uint64_t up0 = bperm64_addr(chv, takeL ? pc.addrL : pc.addrR);
+        const uint64_t fpre = bperm64_addr(L, pc.addrHalf);
+        const uint64_t mv = ballot(!(val > chv));
+        const uint64_t W = pc.path(mv, lm);
+        uint64_t rootv = val;
+        uint32_t last = 64u;
+        if (W) {
+            last = 63u - (uint32_t)__builtin_clzll(W);
+            const uint64_t up = in_mask(1ull << last) ? val : up0;
+            L = in_mask(W & lm) ? up : L;
+            R = in_mask(W & ~lm) ? up : R;
+            rootv = (W & 1ull) ? readlane64(chv, 0) : val;
+        }
+        // heap_push(128, vnew): as push128v2, with the fathers' post-pop values formed locally
+        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
+        constexpr uint64_t kAncL = kHold & ~(1ull << 63);
+        const int h = __builtin_popcountll(ballot(vnew > L) & kAncL) + (sgt64(vnew, rootv) ? 1 : 0);
+        if (h == 0) {
+            L = in_mask(1ull << 63) ? vnew : L;
+            return rootv;
+        }
+        const uint32_t k = (uint32_t)lane >> 1;
+        const bool moved = (((W & lm) >> k) & 1ull) != 0ull;
+        const uint64_t fl = moved ? (k == last ? val : chv) : fpre;
+        const uint64_t mlt = kHold & (~0ull << ((1u << (7 - h)) - 1u));
+        L = in_mask(mlt) ? fl : L;
+        if (h == 7) {
+            L = in_mask(1ull) ? rootv : L;
+            return vnew;
+        }
+        L = in_mask(1ull << ((1u << (6 - h)) - 1u)) ? vnew : L;
         return rootv;
     }
 
@@ -798,6 +851,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
                     v1 = lane < deg0 ? (int32_t)praw.x : -1;
                     c8_pref = lane < deg0 ? make_uint2(praw.y, praw.z) : make_uint2(0u, 0u);
+                    if (STAMPS) { // the row is in registers (its wait covers the previous hop's marks)
+                        const uint32_t tch = __builtin_amdgcn_readfirstlane((uint32_t)v1 ^ c8_pref.x);
+                        st_acc[10] += tch == 0x5A5A5A5Au ? 1u : 0u;
+                        DRM_FSTAMP(10);
+                    }
                 } else if (!hit)
                     load_link(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0, v1, c8_pref);
             } else if (!hit)
@@ -952,7 +1010,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (lo32(root) != kPopLo)
                         --nvalid;
                     if (ef == 128) {
-#if DRM_PQ_HEAPV2
+#if DRM_PQ_HEAPV2 && DRM_PQ_REPL1
+                        root = hp.replace128(val, pconst, lane);
+#elif DRM_PQ_HEAPV2
                         root = hp.push128v2(val, pconst, hp.pop128v2(pconst));
 #else
                         root = hp.push128(val, lane, hp.pop128(lane, pconst));

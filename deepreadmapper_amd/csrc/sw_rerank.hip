@@ -596,7 +596,10 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
     // beside three search waves (8 KB of LUT each) on a CU (co-resident search + rerank)
     constexpr int PPROF = 4 * GST + 5 * PST;
     __shared__ __align__(16) uint32_t pprof[PPROF];
-    __shared__ __align__(16) uint8_t qbuf[(LQ + 15) & ~15];
+    // the query as given (up to LQ + 2 bytes: the tags of a 150 bp read around LQ = 150 DP columns)
+    constexpr int QB = (LQ + 2 + 15) & ~15;
+    __shared__ __align__(16) uint8_t qbuf[QB];
+    __shared__ int lead_s, qe_s;
     __shared__ uint32_t qmask[8]; // bytes present in the query
     extern __shared__ uint32_t cand[]; // [a.cmax]
     __shared__ int ncand_s, flag_s;
@@ -625,20 +628,37 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             // sparse (:238-335) or dynamic lookup: expand, duplicates kept (:502-507)
             ncand_s = find_candidates(a, nb, nsel, cand, a.cmax);
         }
-        for (int t = tid; t < ((LQ + 15) & ~15); t += 64)
-            qbuf[t] = (t < qlen && t < LQ) ? a.queries[q * a.q_stride + t] : 0;
+        for (int t = tid; t < QB; t += 64)
+            qbuf[t] = (t < qlen && t < QB) ? a.queries[q * a.q_stride + t] : 0;
         if (tid < 8)
             qmask[tid] = 0u;
         if (tid == 0)
             flag_s = 0;
         __syncthreads();
-        for (int t = tid; t < qlen && t < LQ; t += 64)
+        for (int t = tid; t < qlen && t < QB; t += 64)
             atomicOr(&qmask[qbuf[t] >> 5], 1u << (qbuf[t] & 31));
+        // Leading and trailing query bytes that are not A/C/G/T (the "<" / ">" tags) are dropped from the DP: on
+        // this path no candidate byte matches them (a candidate byte equal to a non-ACGT query byte flags the query
+        // for the bit-profile kernel), so a leading such column holds 0 in every row -- the zero border the next
+        // column sees anyway -- and a trailing one never exceeds the best of the columns to its left (each of its
+        // cells is a neighbour minus 1, or 0). The DP over the remaining qe columns gives the same score.
+        if (tid == 0) {
+            const int n = qlen < QB ? qlen : QB;
+            int lo = 0, hi = n;
+            while (lo < hi && acgt_code(qbuf[lo]) < 0)
+                ++lo;
+            while (hi > lo && acgt_code(qbuf[hi - 1]) < 0)
+                --hi;
+            lead_s = lo;
+            qe_s = hi - lo;
+        }
+        __syncthreads();
+        const int lead = lead_s, qe = qe_s;
         for (int e = tid; e < PPROF; e += 64) {
             const int ka = e / GST, kb = (e % GST) / PST, j = (e % GST) % PST;
             uint32_t word = 0;
-            if (kb < 5 && j < qlen && j < LQ) {
-                const int c = qbuf[j];
+            if (kb < 5 && j < qe && j < LQ) {
+                const int c = qbuf[lead + j];
                 // the diagonal term: +2 on a match (the -1 every cell takes makes it +1), 2^-9 in the fp16 form
                 const uint32_t t = DRM_SW_INT ? 0x0002u : 0x1800u;
                 word = (c == acgt_byte(ka) ? t : 0u) | (c == acgt_byte(kb) ? t << 16 : 0u);
@@ -646,10 +666,12 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             pprof[e] = word;
         }
         __syncthreads();
-        const int ncand = (qlen > LQ) ? -3 : ncand_s;
-        bool flagged = false;
+        // longer than the buffer: unsupported here (-3); more than LQ columns left after the tags: the bit-profile
+        // kernel scores the query (flagged)
+        const int ncand = (qlen > QB) ? -3 : ncand_s;
+        bool flagged = qe > LQ;
         // two candidates per lane: c and c + 64
-        for (int c0 = tid; c0 < ncand; c0 += 128) {
+        for (int c0 = tid; c0 < (qe > LQ ? 0 : ncand); c0 += 128) {
             const int c1 = c0 + 64;
             const bool has_b = c1 < ncand;
 #if DRM_SW_INT
@@ -912,7 +934,9 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         if (force_bits) {
             hipLaunchKernelGGL((sw_score_kernel<152>), dim3(grid), dim3(64), 0, stream, a);
         } else {
-            hipLaunchKernelGGL((sw_score_f16_kernel<152>), dim3(grid), dim3(64), cand_lds, stream, a);
+            // 150 DP columns: the read's bases; the "<" / ">" tags are dropped in the kernel (a query with more
+            // than 150 columns left after its non-ACGT ends is flagged and scored by the bit-profile kernel)
+            hipLaunchKernelGGL((sw_score_f16_kernel<150>), dim3(grid), dim3(64), cand_lds, stream, a);
             hipLaunchKernelGGL((sw_score_kernel<152, true>), dim3(grid), dim3(64), 0, stream, a);
         }
         break;

@@ -86,6 +86,33 @@ def test_rerank_many_distinct_bytes(c1):
     _rerank_both(refs, nb, reads, 1, 5, 20)
 
 
+def test_rerank_nonacgt_query_ends(c1):
+    """The fp16/int class-profile kernel drops leading and trailing non-ACGT query bytes (the "<" ">" tags) from
+    its DP: reads with such ends of every shape -- tags, runs of N, a read of tags only, 150 / 151 / 152 DNA bytes
+    (more than 150 columns go to the bit-profile kernel) -- against windows with N runs and with "<" / ">" bytes
+    (which must flag the query, since they match its tags) equal the oracle."""
+    rng = np.random.default_rng(33)
+    refs = c1["refs"][:240].copy()
+    refs[10:20, 40:45] = ord("N")
+    refs[30, 0] = ord("<")
+    refs[31, 149] = ord(">")
+    refs[32, 70] = ord(">")
+    dna = lambda n: bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=n).astype(np.uint8))
+    reads = []
+    for i in range(96):
+        body = c1["reads"][i % len(c1["reads"])][1:-1] if i % 3 else dna(int(rng.integers(1, 151)))
+        pre = [b"<", b"", b"N", b"NN<", b"<N", b"X<"][i % 6]
+        post = [b">", b"", b"N", b">>", b"N>", b">X"][(i // 6) % 6]
+        reads.append(pre + body[: 150 - len(pre) - len(post) + 2] + post if len(pre + body + post) > 152 else
+                     pre + body + post)
+    reads += [b"<>", b"<NN>", b"N", dna(150), dna(151), dna(152), b"<" + dna(150), dna(150) + b">", b"<" + dna(150) + b">"]
+    assert max(map(len, reads)) <= 152
+    n = len(reads)
+    nb = rng.integers(0, len(refs), size=(n, 24)).astype(np.int64)
+    nb[:, 0] = 30 + np.arange(n) % 3  # the windows with tag bytes in every list
+    _rerank_both(refs, nb, reads, 1, 24, 24)
+
+
 @pytest.mark.parametrize("stride", [2, 3, 4])
 def test_rerank_sparse_vs_oracle(c1, stride):
     rng = np.random.default_rng(stride)
