@@ -122,7 +122,8 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 #ifndef DRM_PQ_TAGMARK
 // tagged visited words, first mark of a word in a query: 1 = atomic max (generation) then OR (the bit);
 // 0 = plain store then OR (measured 3.7x slower: a store and an atomic to one address back to back);
-// 2 = OR only (diagnostic: wrong once a word carries an older generation)
+// 2 = OR only (diagnostic: wrong once a word carries an older generation); 3 = max or OR, one atomic per link
+// (timing diagnostic: wrong when two fresh links of one row share a stale word)
 #define DRM_PQ_TAGMARK 1
 #endif
 
@@ -939,7 +940,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if ((old >> 16) != gen)
                     __hip_atomic_fetch_max(&vis[v1 >> 4], gen << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
+#if DRM_PQ_TAGMARK == 3
+                // timing diagnostic only (inexact when two fresh links of a row share a stale word): one atomic per link
+                if ((old >> 16) != gen)
+                    __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
                 __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
             } else if (use_spec && fresh) // the test was a load: mark the fresh links
                 __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             DRM_FSTAMP(3);

@@ -199,21 +199,24 @@ __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *c
                 u[i] = ca[i];
                 w[i] = cb[i];
             }
-            float acc0 = 0.0f, acc1 = 0.0f;
+            // the two entries' chains side by side in the halves of packed fp32 ops (v_pk_add_f32 / v_pk_mul_f32):
+            // each entry keeps its own sequence of IEEE round-to-nearest subtract, multiply, add (no contraction)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            f2 acc = {0.0f, 0.0f};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float cu[4] = {u[i].x, u[i].y, u[i].z, u[i].w};
                 const float cw[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float d0 = __fsub_rn(xs[4 * i + j], cu[j]);
-                    const float d1 = __fsub_rn(xs[4 * i + j], cw[j]);
-                    acc0 = __fadd_rn(acc0, __fmul_rn(d0, d0));
-                    acc1 = __fadd_rn(acc1, __fmul_rn(d1, d1));
+                    const f2 x2 = {xs[4 * i + j], xs[4 * i + j]};
+                    const f2 c2 = {cu[j], cw[j]};
+                    const f2 d = x2 - c2;
+                    acc = acc + d * d;
                 }
             }
-            lut[e0] = acc0;
-            lut[e0 + 64] = acc1;
+            lut[e0] = acc.x;
+            lut[e0 + 64] = acc.y;
         }
     }
     __syncthreads();
