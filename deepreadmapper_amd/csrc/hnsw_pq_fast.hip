@@ -120,6 +120,8 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 #endif
 
 #ifndef DRM_PQ_TAGMARK
+// 4: one atomic per fresh link (max on a stale word, returning; OR on a current one), the rare links that
+// found their word restarted by another link of the same row repaired at the next hop (see the hop loop)
 // tagged visited words, first mark of a word in a query: 1 = atomic max (generation) then OR (the bit);
 // 0 = plain store then OR (measured 3.7x slower: a store and an atomic to one address back to back);
 // 2 = OR only (diagnostic: wrong once a word carries an older generation); 3 = max or OR, one atomic per link
@@ -798,6 +800,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // INL: a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row
         // prediction can skip links back to nodes already expanded before the visited test has answered
         uint32_t popped_bits = 0u;
+        // DRM_PQ_TAGMARK == 4: the previous hop's restart marks -- lanes that issued one, the value each found, its id
+        uint64_t mstale = 0;
+        uint32_t mret = 0u;
+        int32_t mprev = -1;
         Link3 praw{0xFFFFFFFFu, 0u, 0u}; // DRM_PQ_ASYNC: the predicted row's link `lane`, raw (pred = -1: none yet)
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
         while (nvalid > 0) {
@@ -918,7 +924,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 }
             }
             // visited in this query: (tagged) the word carries this query's generation and the node's bit
-            const bool seen = INL ? ((old >> 16) == gen && (old & bit) != 0u) : (old & bit) != 0u;
+            bool seen = INL ? ((old >> 16) == gen && (old & bit) != 0u) : (old & bit) != 0u;
+#if DRM_PQ_TAGMARK == 4
+            // the previous hop's restart marks (one returning atomic max per fresh link on a stale word): a link that
+            // found its word already restarted in that same instruction (a "follower": another fresh link of the row
+            // shares the word) may have lost its bit in the max, or dropped the bits it found -- it now ORs back the
+            // word it saw plus its own bit, so every bit of the group ends up set. This row's visited load was issued
+            // before that repair, so a link whose word is a follower's and whose bit is in what the follower saw or
+            // its own bit counts as visited (any such bit is this query's). Followers are rare: the branch is
+            // usually not taken.
+            if (INL && mstale) {
+                const uint64_t F = ballot(((mstale >> lane) & 1ull) && (mret >> 16) == gen);
+                if (F) {
+                    const uint32_t fix = mret | (gen << 16) | (1u << (mprev & 15));
+                    if ((F >> lane) & 1ull)
+                        __hip_atomic_fetch_or(&vis[mprev >> 4], fix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    for (uint64_t f = F; f; f &= f - 1) {
+                        const int fl = __builtin_ctzll(f);
+                        const int32_t fw = __builtin_amdgcn_readlane(mprev, fl) >> 4;
+                        const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)fix, fl);
+                        seen = seen || (act && (v1 >> 4) == fw && ((fb >> (v1 & 15)) & 1u) != 0u);
+                    }
+                }
+            }
+#endif
             bool fresh = act && !seen;
             if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
@@ -946,11 +975,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else
                     __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#elif DRM_PQ_TAGMARK == 4
+                // one atomic per fresh link: a stale word is restarted with this link's bit by an atomic max (the first
+                // lane of the instruction to reach the word wins; the returned value tells the others, repaired at
+                // the next hop); a word of this generation takes the bit by an OR
+                if ((old >> 16) != gen)
+                    mret = __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
                 __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
             } else if (use_spec && fresh) // the test was a load: mark the fresh links
                 __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if DRM_PQ_TAGMARK == 4
+            if (INL) {
+                mstale = ballot(fresh && (old >> 16) != gen);
+                mprev = v1;
+            }
+#endif
             DRM_FSTAMP(3);
             fm = check_dups ? ballot(fresh) : ballot(!seen) & actm;
             const int nf = __builtin_popcountll(fm);
