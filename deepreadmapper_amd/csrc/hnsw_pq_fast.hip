@@ -125,7 +125,8 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 // tagged visited words, first mark of a word in a query: 1 = atomic max (generation) then OR (the bit);
 // 0 = plain store then OR (measured 3.7x slower: a store and an atomic to one address back to back);
 // 2 = OR only (diagnostic: wrong once a word carries an older generation); 3 = max or OR, one atomic per link
-// (timing diagnostic: wrong when two fresh links of one row share a stale word)
+// (timing diagnostic: wrong when two fresh links of one row share a stale word); 5 = one atomic per link unless two
+// fresh links of the row share a stale word (checked exactly per row; then the two-atomic form)
 #define DRM_PQ_TAGMARK 1
 #endif
 
@@ -949,6 +950,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
 #endif
             bool fresh = act && !seen;
+#if DRM_PQ_TAGMARK == 5
+            bool mshared = false; // two fresh links of this row on one stale word (decided after check_dups below)
+#endif
             if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
                     const int32_t vj = __shfl(v1, j, 64);
@@ -956,6 +960,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         fresh = false;
                 }
             }
+#if DRM_PQ_TAGMARK == 5
+            if (INL) {
+                const uint64_t S = ballot(fresh && (old >> 16) != gen);
+                const uint32_t wv = (uint32_t)v1 >> 4;
+                for (uint64_t rest = S; rest;) {
+                    const uint32_t wl = (uint32_t)__builtin_amdgcn_readlane((int)wv, __builtin_ctzll(rest));
+                    const uint64_t same = ballot(wv == wl) & S;
+                    if (same & (same - 1)) {
+                        mshared = true;
+                        break;
+                    }
+                    rest &= ~same;
+                }
+            }
+#endif
             if (INL && fresh) {
                 // mark the fresh links: a word still carrying an older generation is restarted with this one
                 // (atomic max with gen << 16: generations only grow between wraps, so the max drops the old tag
@@ -975,6 +994,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else
                     __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#elif DRM_PQ_TAGMARK == 5
+                // one atomic per fresh link unless two fresh links of this row share a stale word (checked exactly
+                // over the stale words below, wave-uniform): then the two-atomic form for the row
+                if (!mshared) {
+                    if ((old >> 16) != gen)
+                        __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else
+                        __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    if ((old >> 16) != gen)
+                        __hip_atomic_fetch_max(&vis[v1 >> 4], gen << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
 #elif DRM_PQ_TAGMARK == 4
                 // one atomic per fresh link: a stale word is restarted with this link's bit by an atomic max (the first
                 // lane of the instruction to reach the word wins; the returned value tells the others, repaired at
