@@ -7,19 +7,17 @@ of synthetic 150 bp reads, inputs already resident in HBM: the HNSW search kerne
 rerank kernel (post_process_sw_static(..., k=K, k_clusters=K), src/main.cpp:340). Rank 0 prints ONE
 JSON line.
 
-Search (`--index`):
-  flat (default): BASELINE.json configs[1]'s "HIP L2 HNSW search" -- hnswlib fp32-L2 searchKnn
-      (search(index, queries, k, ef), src/hnswlib_dir/search.cpp:7-52) on an hnswlib index with the
-      reference's defaults M=64, EFC=128 (src/hnswlib_dir/index.cpp); the distance kernel whose HBM
-      roofline the north star quotes (512 B per distance).
-  pq: faiss IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200, built here since faiss is absent) through
-      faiss_search(index, emb, k_clusters=K, ef=EF) (src/main.cpp:278), the live pipeline's index.
+Workload (`--workload`, default c5): BASELINE.json configs[4], the configuration the 1/2/4/8-GPU metric is
+quoted on, per GPU: a seeded 25,000,149 bp genome -> 50,000,000 stride-1 fwd/RC 150 bp windows, a GPU-built
+faiss IndexHNSWPQ (M_pq=8 nbits=8 M_hnsw=16 EFC=200; faiss is absent), 1.25M reads per GPU (weak scaling:
+rank r searches its own contiguous shard of one seeded read stream), windows and reads embedded by the
+reference's GRU model on the GPU (`--embed kmer3`: the 3-mer stand-in). c3: 1M windows, 100k reads; c4: the
+10M-window stride-4 index, search only at K = 128 and 5.
 
-Workload (BASELINE.json configs[2] "C3", the HBM-roofline run): a seeded 500,149
-bp genome, stride-1 dense window table of 1,000,000 fwd/RC 150 bp windows, 100,000 reads per GPU (1 %
-substitutions; weak scaling: the per-GPU batch is fixed). Queries are embedded with the 3-mer
-stand-in (the OpenVINO encoder is out of scope); the reference's timed "Search time" window likewise
-excludes inference (src/main.cpp:272-285).
+Search (`--index`): pq (default), faiss_search(index, emb, k_clusters=K, ef=EF) (src/main.cpp:278), the live
+pipeline's index; flat (C3 only): hnswlib fp32-L2 searchKnn (src/hnswlib_dir/search.cpp:7-52), M=64, EFC=128.
+The timed region excludes inference and file I/O, as the reference's "Search time" window does
+(src/main.cpp:272-285); the encoder, the L2 rerank and the PCIe-inclusive host path are reported beside it.
 """
 import argparse
 import json
@@ -34,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
-SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, true>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline codes) launch (hnsw_pq_fast.hip)
+SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, false>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline rows) launch (hnsw_pq_fast.hip)
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<150>"  # 150 DP columns: a tagged 150 bp read without its "<" / ">" ends
 SW_VALU_PER_CELL_PAIR = 1053 / 300  # static ISA count of sw_score_f16_kernel<150>'s two-row block: 1053 VALU per 2 x 150 cell pairs
@@ -370,8 +368,8 @@ def gather_results(D, dev, n_total, bufs, local_host):
     """End-of-run exchange: every rank's device-resident result rows are gathered to
     rank 0 over RCCL by the library's own C++ path (drm_comm_gather_rows: grouped ncclSend/ncclRecv over
     xGMI), outside the timed region; the RCCL unique id travels over the gloo control plane. Rank 0
-    checks its own shard in the gathered rows. Reported, never fatal: the scaling numbers stand either
-    way."""
+    checks its own shard in the gathered rows. An exception is returned as {"error": ...}: gather_verdict
+    turns it into a failed job."""
     if D.world == 1:
         return None
     from deepreadmapper_amd.device import device_count
@@ -406,6 +404,23 @@ def gather_results(D, dev, n_total, bufs, local_host):
         return out
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def gather_verdict(D, gather):
+    """N > 1: did the end-of-run RCCL gather work on every rank? True / False, or None when there is nothing to
+    check (one rank, or ranks sharing a device, where RCCL cannot run). Every rank reaches the same answer (sums
+    over ranks of failure and skip flags on the gloo control plane), so a broken gather fails the whole job: the
+    JSON line carries `gather_ok` and the bench exits non-zero."""
+    if D.world == 1:
+        return None
+    skipped = gather is not None and "skipped" in gather
+    bad = not skipped and (gather is None or "error" in gather or
+                           (D.rank == 0 and not gather.get("rank0_shard_matches", False)))
+    n_bad = D.allreduce(1.0 if bad else 0.0, "SUM")
+    n_skip = D.allreduce(1.0 if skipped else 0.0, "SUM")
+    if n_bad > 0:
+        return False
+    return None if n_skip > 0 else True
 
 
 def run_c4(args, D):
@@ -455,6 +470,11 @@ def run_c4(args, D):
         synchronize()
         el = D.allreduce(time.perf_counter() - t0, "MAX")
         ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in ev]))
+        # faiss's ndis for the algorithmic bytes: one untimed exact-statistics search (see main())
+        ix.set_exact_stats(True)
+        ix.search_device(d_x, Q, K, args.ef, d_D, d_I, d_nd, d_nh, stream, d_nhops_upper=d_nu)
+        stream.synchronize()
+        ix.set_exact_stats(False)
         ndis, nhops, nup = d_nd.download().astype(np.int64), d_nh.download().astype(np.int64), d_nu.download()
         code = (info.pq_M * info.pq_nbits + 7) // 8
         bytes_q = 4 * info.d + (nhops - nup) * 2 * info.M_hnsw * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
@@ -660,6 +680,22 @@ def main():
     if not (st == K).all():
         raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")
     ndis, nhops, nup = d_nd.download().astype(np.int64), d_nh.download().astype(np.int64), d_nu.download()
+    if (nhops < 0).any():
+        raise SystemExit(f"{int((nhops < 0).sum())} queries ended on the search's hop bound")
+    ndis_computed = ndis
+    if not flat:
+        # faiss's ndis (the links each hop finds not yet visited: SURVEY.md sec. 8d's algorithmic bytes) from one
+        # untimed exact-statistics search of the same reads (a visited bitmap kept beside the search only for the
+        # count); the lean kernel's own ndis counts every distance it computed. Its rows must equal the timed run's.
+        I_timed = d_I.download()
+        ix.set_exact_stats(True)
+        ix.search_device(d_x, Q, K, EF, d_D, d_I, d_nd, d_nh, stream, d_nhops_upper=d_nu)
+        stream.synchronize()
+        ix.set_exact_stats(False)
+        if not np.array_equal(d_I.download(), I_timed):
+            raise SystemExit("the exact-statistics search returned different rows")
+        ndis = d_nd.download().astype(np.int64)
+        del I_timed
     ids = d_id.download()
     top1 = float(np.mean(ids[:, 0].astype(np.int64) == truth))
     intop = float(np.mean((ids.astype(np.int64) == truth[:, None]).any(axis=1)))
@@ -717,6 +753,7 @@ def main():
     value = total_reads / elapsed_max
     gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_L if flat else d_I),
                                            ("search_dists", d_D)], {"sw_ids": ids})
+    gather_ok = gather_verdict(D, gather)
     result = None
     if D.rank == 0:
         cpu = None
@@ -762,6 +799,7 @@ def main():
                                     "cell pair is reported separately"},
             "cpu_baseline": cpu,
             "gather": gather,
+            "gather_ok": gather_ok,
             "host_path": host,
             "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
             if enc else None,
@@ -773,12 +811,15 @@ def main():
                           "first_search_alone_ms": round(first_search_ms, 3), "last_sw_alone_ms": round(last_sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
+                          "distances_computed_mean": round(float(ndis_computed.mean()), 1),
                           "bytes_per_query": round(float(bytes_q.mean()), 1),
                           "tie_fallback_queries": n_fallback,
                           "truth_top1": round(top1, 4), "truth_in_topk": round(intop, 4)},
         }
         emit(result)
     D.close()
+    if gather_ok is False:
+        raise SystemExit(f"rank {D.rank}: the RCCL result gather failed on some rank ({gather})")
 
 
 if __name__ == "__main__":

@@ -18,6 +18,7 @@ DRM_ERR_HIP = -4
 DRM_ERR_CANDS = -5
 DRM_ERR_K = -6
 DRM_ERR_UNSUPPORTED = -7
+DRM_ERR_INTERNAL = -8
 
 # Every symbol include/drm_hip.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = [
@@ -41,6 +42,7 @@ EXPORTS = [
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
     "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
     "drm_index_set_search_waves", "drm_refs_set_sw_waves", "drm_search_rerank_device",
+    "drm_index_set_exact_stats",
 ]
 
 
@@ -114,6 +116,7 @@ def lib():
         "drm_index_free": (C.c_int, [vp]),
         "drm_index_get_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
         "drm_index_set_search_waves": (C.c_int, [vp, i32]),
+        "drm_index_set_exact_stats": (C.c_int, [vp, i32]),
         "drm_refs_set_sw_waves": (C.c_int, [vp, i32]),
         "drm_search_rerank_device": (C.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
                                                vp, vp, vp, vp, C.POINTER(PipelineStats)]),
@@ -182,7 +185,11 @@ def lib():
         "drm_post_process_l2_dynamic_device": (C.c_int, [vp, vp, i64, i32, vp, i32, i64, i32, i32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:
+            if os.environ.get("DRM_LIB"):  # an A/B build of an older ABI: bind what it has
+                continue
+            raise ImportError(f"{LIB_PATH} does not export {name}")
         f.restype = res
         f.argtypes = args
     _lib = L

@@ -83,8 +83,7 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 void free_index(drm::DeviceIndex &d)
 {
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
-                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes,
-                    d.vis_tag,    d.vis_gen};
+                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -250,6 +249,9 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.force_exact = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
+        d.waves_per_cu_load = d.waves_per_cu;
+        if (const char *e = std::getenv("DRM_SEARCH_EXACT_STATS"))
+            d.exact_stats = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LOG_CAP"))
             d.log_cap_req = std::max(1, std::atoi(e));
         if (const char *e = std::getenv("DRM_SEARCH_FAST"))
@@ -314,26 +316,6 @@ int drm_debug_search_stamps(drm_index *index, uint64_t *out12)
     });
 }
 
-// Test hook: restart every slot's visited words at the given generation (the inline-row kernel's tag), e.g. just
-// below the 16-bit wrap, so that a test sees the slots zero their words mid-batch
-int drm_debug_search_generation(drm_index *index, uint32_t generation)
-{
-    return guarded([&] {
-        if (!index || !index->dev.vis_gen)
-            throw Error(DRM_ERR_ARG, "index has no tagged visited words (inline rows off)");
-        if (generation > 0xFFFFu)
-            throw Error(DRM_ERR_ARG, "generation must be <= 0xFFFF");
-        DRM_HIP_CHECK(hipSetDevice(index->dev.device));
-        DRM_HIP_CHECK(hipDeviceSynchronize());
-        // generations only ever increase between wraps: a word's tag must never reappear for a later query, so
-        // the words restart from zero with the new generation
-        DRM_HIP_CHECK(hipMemset(index->dev.vis_tag, 0,
-                                sizeof(uint32_t) * (size_t)index->dev.tag_slots * (size_t)index->dev.tag_words));
-        std::vector<uint32_t> g((size_t)index->dev.tag_slots, generation);
-        DRM_HIP_CHECK(hipMemcpy(index->dev.vis_gen, g.data(), g.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    });
-}
-
 int drm_search_fallbacks(drm_index *index, int64_t *count)
 {
     return guarded([&] {
@@ -354,8 +336,17 @@ int drm_index_set_search_waves(drm_index *index, int32_t waves_per_cu)
         if (!index || waves_per_cu < 0)
             throw Error(DRM_ERR_ARG, "invalid argument");
         // the per-slot workspace was reserved at load for index->dev.waves_per_cu; more slots grow it on
-        // the next search, fewer use a prefix of it
-        index->dev.waves_per_cu = waves_per_cu > 0 ? waves_per_cu : 20;
+        // the next search, fewer use a prefix of it; 0 restores the value the index was loaded with
+        index->dev.waves_per_cu = waves_per_cu > 0 ? waves_per_cu : index->dev.waves_per_cu_load;
+    });
+}
+
+int drm_index_set_exact_stats(drm_index *index, int32_t on)
+{
+    return guarded([&] {
+        if (!index)
+            throw Error(DRM_ERR_ARG, "null index");
+        index->dev.exact_stats = on ? 1 : 0;
     });
 }
 
@@ -441,6 +432,7 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
         DRM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+        drm::check_search_errors(index->dev);
         dD.download(D);
         dI.download(I);
         if (stats) {

@@ -55,6 +55,8 @@ struct DeviceIndex {
     int32_t force_exact = 0;   // skip the sorted-array pass (every query through the exact kernel)
     int32_t try_sorted = 0;    // run the sorted-array pass first (DRM_SEARCH_SORTED=1)
     int32_t waves_per_cu = 20; // resident search waves per CU (LDS allows 20 at 8 KB of LUT each)
+    int32_t waves_per_cu_load = 20; // the value set at load (DRM_SEARCH_WAVES_PER_CU or 20): what 0 restores
+    int32_t exact_stats = 0;   // lean kernel: count faiss's ndis with a visited bitmap (DRM_SEARCH_EXACT_STATS)
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
@@ -77,20 +79,15 @@ struct DeviceIndex {
     uint32_t *visited = nullptr;   // [n_slots][vis_words]
     int32_t clear_cap = 0;
     int32_t *clear_list = nullptr; // [n_slots][clear_cap]
-    uint32_t *counter = nullptr;   // [0] work queue head, [1] fallback count, [2] fallback queue head
+    uint32_t *counter = nullptr;   // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] errors
     int32_t *fb_list = nullptr;    // queries the sorted-array pass handed to the exact kernel
     int64_t fb_cap = 0;
     int32_t use_fast = 1;          // lean kernel (hnsw_pq_fast.hip) where it applies; DRM_SEARCH_FAST=0 off
     uint64_t *log = nullptr;       // [n_slots][log_cap] accepted pushes (lean kernel, k == ef)
     int32_t log_cap = 0, log_slots = 0;
     int32_t log_cap_req = 2048;    // entries per slot (DRM_SEARCH_LOG_CAP; >= ef + 64, compaction beyond)
-    // inline-row lean kernel: generation-tagged visited words, 16 node bits | (query generation << 16) each,
-    // never cleared per query (a new generation per query; a slot zeroes its words at the 16-bit wrap). The
-    // plain bitmap above is then allocated only if another kernel runs
-    int32_t tag_slots = 0;
-    int64_t tag_words = 0;         // words per slot: ceil(ntotal / 16), a multiple of 4
-    uint32_t *vis_tag = nullptr;   // [tag_slots][tag_words]
-    uint32_t *vis_gen = nullptr;   // [tag_slots] each slot's last generation
+    // the lean kernel keeps no visited table (its heap is the visited set): the bitmap above
+    // is allocated only for the other kernels, or for exact_stats
     int64_t device_bytes = 0;
     HnswPqHost meta; // header fields kept for drm_index_get_info (vectors released)
 };
@@ -118,7 +115,7 @@ struct SearchArgs {
     int64_t vis_words;
     int32_t *clear_list;
     int32_t clear_cap;
-    uint32_t *counter;
+    uint32_t *counter;     // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] error count
     int32_t check_dups;
     int32_t x_aligned16; // queries 16-B aligned: float4 loads in the LUT build
     uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1), else null
@@ -131,16 +128,18 @@ struct SearchArgs {
     const int32_t *rows;   // lean kernel, inline layout: [ntotal][row_words] ids + codes (DeviceIndex::rows)
     int32_t row_words;
     const uint2 *upper_codes; // lean kernel, inline layout: codes beside upper_nbr (DeviceIndex::upper_codes)
-    uint32_t *vis_gen;        // lean kernel, inline layout: per-slot generations; `visited` is then vis_tag
+    int32_t exact_stats;      // lean kernel: faiss's ndis counted with `visited` (else the distances computed)
 };
 
-// lean kernel (hnsw_pq_fast.hip): PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64
+// lean kernel (hnsw_pq_fast.hip): inline rows, PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc);
-void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream);
+void launch_hnsw_pq_fast(const SearchArgs &a, int slots, bool stamps, hipStream_t stream);
 // DeviceIndex::rows from nbr0 + codes (PQ 8 x 8, deg0 <= 64), on the device
 void build_inline_rows(DeviceIndex &ix);
 
 void reserve_search_scratch(DeviceIndex &ix);
+// after a synchronised search: DRM_ERR_INTERNAL if a query of it ended on the hop bound (counter[3])
+void check_search_errors(const DeviceIndex &ix);
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
@@ -206,7 +205,7 @@ struct FlatArgs {
     int64_t vis_words;
     int32_t *clear_list;
     int32_t clear_cap;
-    uint32_t *counter;
+    uint32_t *counter;     // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] error count
     int32_t check_dups;
     int32_t cand_lds;
     float *cand_ovf_k;

@@ -4,20 +4,25 @@
 // search_from_candidates with MinimaxHeap + HeapBlockResultHandler [upstream faiss >= 1.8],
 // restated in oracle/drm_oracle.c). Caller: faiss_search (src/hnswpq/search.cpp:39-40).
 //
-// What makes it lean (DESIGN.md sec. 4, "hnsw_pq_fast_kernel"):
+// What makes it lean (DESIGN.md sec. 4.1, "hnsw_pq_fast_kernel"):
 //   * every MinimaxHeap slot is one u64 = (ord32(distance) << 32) | (id ^ 2^31): faiss's cmp2 on
 //     (distance, id) -- popped slots carry id -1 -- becomes a single unsigned 64-bit compare;
 //   * the heap sits in the sibling-pair layout (lane p holds the children of node p, slots 2p+1 and
-//     2p+2; the root is lane 63's second half). heap_pop finds the sift-down path by pointer doubling
-//     (3 ds_bpermute) and heap_push the sift-up chain by one parallel ancestor fetch: no scalar walks;
+//     2p+2; the root is lane 63's second half); a full-heap replace finds its sift-down path from two
+//     ballots and per-lane ancestor masks, and its sift-up chain by one parallel compare;
 //   * pop_min is one 32-bit DPP min plus a ballot for the highest tied slot;
 //   * result set at k == ef: the HeapBlockResultHandler (k = ef) holds, at every step, the same
-//     multiset of distances as the MinimaxHeap (both start empty, both accept everything until they
-//     hold ef entries, then both take d < (their common) maximum and drop one maximum). Its final
-//     content is therefore the k smallest (distance, id) pairs among the pushes the MinimaxHeap
-//     accepted, with the MinimaxHeap's final root distance T as the k-th distance. The kernel logs
-//     every accepted push (one masked store per hop) instead of maintaining the result heap, and
-//     selects + sorts the k results once per query. k < ef keeps a register result set (k <= 64).
+//     multiset of distances as the MinimaxHeap, so the kernel logs every accepted push and selects +
+//     sorts the k results once per query. k < ef keeps a register result set (k <= 64);
+//   * no visited table. faiss's VisitedTable answers "was this link seen before?"; the kernel answers it
+//     from the heap instead ("The heap is the visited set"). Every heap slot also
+//     carries its node id (IL / IR), popped or not. A link whose distance is at or above the root of the
+//     full heap is rejected by MinimaxHeap::push whether it was seen or not (the root only falls), and a
+//     seen link below that root has never left the heap; so "seen" == "in the heap" wherever it decides
+//     anything, and the same pushes are accepted in the same order as with faiss's table. The hop's only
+//     memory access is its level-0 row (ids + codes inline), predicted and fetched one hop ahead.
+//     ndis (faiss's count of never-seen links) needs the table: the STATS instantiation keeps a plain
+//     bitmap beside the heap for the count only (drm_index_set_exact_stats).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,6 +47,7 @@ __device__ __forceinline__ uint64_t pack(uint32_t key, int32_t id)
 __device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
 __device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
 __device__ __forceinline__ int32_t unpack_id(uint64_t v) { return (int32_t)(lo32(v) ^ 0x80000000u); }
+__device__ __forceinline__ int32_t readlane32(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 {
     const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hi32(v), l);
@@ -56,7 +62,11 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, int src)
 {
     return ((uint64_t)bperm32(hi32(v), src) << 32) | bperm32(lo32(v), src);
 }
-__device__ __forceinline__ uint64_t bperm64_addr(uint64_t v, uint32_t addr) // addr = source lane * 4
+__device__ __forceinline__ int32_t bperm32_addr(int32_t v, uint32_t addr) // addr = source lane * 4
+{
+    return __builtin_amdgcn_ds_bpermute((int)addr, v);
+}
+__device__ __forceinline__ uint64_t bperm64_addr(uint64_t v, uint32_t addr)
 {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)hi32(v)) << 32) |
            (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)lo32(v));
@@ -115,35 +125,6 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
     return ord32(r);
 }
 
-#ifndef DRM_PQ_HEAPV2
-#define DRM_PQ_HEAPV2 1 // pop128v2 / push128v2 (requires DRM_PQ_SROOT)
-#endif
-
-#ifndef DRM_PQ_TAGMARK
-// 4: one atomic per fresh link (max on a stale word, returning; OR on a current one), the rare links that
-// found their word restarted by another link of the same row repaired at the next hop (see the hop loop)
-// tagged visited words, first mark of a word in a query: 1 = atomic max (generation) then OR (the bit);
-// 0 = plain store then OR (measured 3.7x slower: a store and an atomic to one address back to back);
-// 2 = OR only (diagnostic: wrong once a word carries an older generation); 3 = max or OR, one atomic per link
-// (timing diagnostic: wrong when two fresh links of one row share a stale word); 5 = one atomic per link unless two
-// fresh links of the row share a stale word (checked exactly per row; then the two-atomic form)
-#define DRM_PQ_TAGMARK 1
-#endif
-
-#ifndef DRM_PQ_REPL1
-#define DRM_PQ_REPL1 1 // full-heap replace as one routine with one cross-lane round trip (Heap::replace128)
-#endif
-
-#ifndef DRM_PQ_SROOT
-// ef = 128 replace pushes keep the root (slot 0) in scalar registers only; lane 63's R is refreshed once per hop
-#define DRM_PQ_SROOT 1
-#endif
-
-
-#ifndef DRM_PQ_VPATH
-#define DRM_PQ_VPATH 1 // pop128's sift-down path by per-lane ancestor masks (0: scalar walk)
-#endif
-
 // Per-lane constants of node p = lane: A = p and its ancestors, Aup = its ancestors, Lreq = the
 // ancestors whose path toward p takes the left child (2a + 1).
 struct PathConst {
@@ -182,11 +163,14 @@ struct PathConst {
     }
 };
 
-// MinimaxHeap arrays (ef <= 128) in the sibling-pair layout.
+// MinimaxHeap arrays (ef <= 128) in the sibling-pair layout. L / R are the faiss keys (a popped slot's id is -1
+// there, as in faiss's ids[] array); IL / IR hold each slot's node id, popped or not (-1: never filled), and move
+// with their keys through every sift. They are what the kernel's visited test reads.
 struct Heap {
     uint64_t L, R;
+    int32_t IL, IR;
 
-    // value of slot s (wave-uniform s)
+    // value / node id of slot s (wave-uniform s)
     __device__ __forceinline__ uint64_t get(int s) const
     {
         if (s == 0)
@@ -194,16 +178,27 @@ struct Heap {
         const int o = (s - 1) >> 1;
         return (s & 1) ? readlane64(L, o) : readlane64(R, o);
     }
+    __device__ __forceinline__ int32_t get_id(int s) const
+    {
+        if (s == 0)
+            return readlane32(IR, 63);
+        const int o = (s - 1) >> 1;
+        return (s & 1) ? readlane32(IL, o) : readlane32(IR, o);
+    }
+    // node v is in the heap (one compare per half, wave-uniform answer)
+    __device__ __forceinline__ bool holds(int32_t v) const { return (ballot(IL == v) | ballot(IR == v)) != 0ull; }
 
     // faiss heap_pop<CMax<float, int>>(k): slot k-1 sifted down from the root (1-based k >= 1).
     __device__ __forceinline__ void pop(int k, int lane)
     {
         const uint64_t val = get(k - 1);
+        const int32_t valI = get_id(k - 1);
         const bool has_l = 2 * lane + 1 <= k - 1;
         const bool has_r = 2 * lane + 2 <= k - 1 && lane != 63;
         const bool takeL = !has_r || L > R;                 // (i2 == k + 1) || cmp2(heap[i1], heap[i2])
         const int ch = takeL ? 2 * lane + 1 : 2 * lane + 2; // chosen child slot
         const uint64_t chv = takeL ? L : R;
+        const int32_t chI = takeL ? IL : IR;
         const bool moves = has_l && !(val > chv);           // the child moves up unless cmp2(val, child)
         // next hole position, pointer-doubled: n8(0) is the final hole (depth <= 7)
         const int n1 = moves ? ch : lane;
@@ -219,185 +214,141 @@ struct Heap {
         const int sh = bitlen(hx) - bitlen((uint32_t)lane + 1u);
         const bool writer = sh > 0 && (hx >> sh) == (uint32_t)lane + 1u;
         const uint64_t up = bperm64(chv, ch & 63);
-        const uint64_t nv = (ch == hole) ? val : up;
-        if (writer && takeL)
+        const int32_t upI = (int32_t)bperm32((uint32_t)chI, ch & 63);
+        const bool at_hole = ch == hole;
+        const uint64_t nv = at_hole ? val : up;
+        const int32_t nvI = at_hole ? valI : upI;
+        if (writer && takeL) {
             L = nv;
-        if (writer && !takeL)
+            IL = nvI;
+        }
+        if (writer && !takeL) {
             R = nv;
-        const uint64_t rootv = hole != 0 ? readlane64(chv, 0) : val;
-        if (lane == 63)
+            IR = nvI;
+        }
+        const bool root_moved = hole != 0;
+        const uint64_t rootv = root_moved ? readlane64(chv, 0) : val;
+        const int32_t rootI = root_moved ? readlane32(chI, 0) : valI;
+        if (lane == 63) {
             R = rootv;
+            IR = rootI;
+        }
     }
 
-    // heap_pop(128) on the full ef = 128 heap: the last slot (127) is lane 63's L. The max-child
-    // path is walked on the scalar unit over two ballots (which child each node takes, whether it
-    // moves up) -- a few SALU cycles per level instead of a chain of cross-lane round trips -- while
-    // the one ds_bpermute that fetches the moving values is already in flight.
-    // returns the new root (slot 0), wave-uniform
-    __device__ __forceinline__ uint64_t pop128(int lane, const PathConst &pc)
+    // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
+    __device__ __forceinline__ void push(int k, uint64_t val, int32_t valI, int lane)
     {
-        const uint64_t val = readlane64(L, 63);
-        const bool takeL = lane == 63 || L > R;
-        const int ch = takeL ? 2 * lane + 1 : 2 * lane + 2;
-        const uint64_t chv = takeL ? L : R;
-        const uint64_t up = bperm64(chv, ch & 63);
-        // ballots of single compares (a ballot of a compound condition costs two extra VALU to
-        // re-materialise the lane mask); lane 63 always takes its L (slot 127 has no sibling)
-        const uint64_t lm = ballot(L > R) | (1ull << 63), mv = ballot(!(val > chv));
-#if DRM_PQ_VPATH
-        // node p is on the sift-down path (its chosen child moves up) iff p and all its ancestors have
-        // mv set and every ancestor chose the child toward p: one test per lane against its constant
-        // ancestor masks, instead of a 7-step scalar walk
-        const uint64_t W = pc.path(mv, lm);
-        uint32_t hole = 0;
-        if (W) {
-            const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
-            hole = 2u * last + 2u - (uint32_t)((lm >> last) & 1ull);
-        }
-#else
-        uint64_t W = 0;
-        uint32_t hole = 0;
-#pragma unroll
-        for (int d = 0; d < 7; ++d) {
-            if (hole >= 64u || !((mv >> hole) & 1ull))
-                break;
-            W |= 1ull << hole;
-            hole = 2u * hole + 2u - (uint32_t)((lm >> hole) & 1ull);
-        }
-#endif
-        const bool writer = (W >> lane) & 1ull;
-        const uint64_t nv = (uint32_t)ch == hole ? val : up;
-        if (writer && takeL)
+        // lane j in [1, 7] looks at the ancestor a_j = k >> j (1-based)
+        const int aj = (lane >= 1 && lane < 8) ? (k >> lane) : 0;
+        const int t = aj - 1; // its slot
+        const int owner = t <= 0 ? 63 : (t - 1) >> 1;
+        const bool sideR = t <= 0 || !(t & 1);
+        const uint64_t fl = bperm64(L, owner), fr = bperm64(R, owner);
+        const int32_t flI = (int32_t)bperm32((uint32_t)IL, owner), frI = (int32_t)bperm32((uint32_t)IR, owner);
+        const uint64_t av = sideR ? fr : fl;
+        const int32_t avI = sideR ? frI : flI;
+        const bool moves = aj >= 1 && val > av; // cmp2(val, father): the father moves down
+        const int h = __builtin_popcountll(ballot(moves)); // ancestors 1..h move (heap order: a prefix)
+        // chain index m (a_m = k >> m, m = 0..h) gets a_{m+1}'s value, or val at m == h
+        const int bk = bitlen((uint32_t)k);
+        const uint32_t xl = 2u * (uint32_t)lane + 2u, xr = xl + 1u; // 1-based indices of L, R
+        const int ml = bk - bitlen(xl), mr = bk - bitlen(xr);
+        const bool onL = ml >= 0 && ml <= h && (uint32_t)(k >> ml) == xl;
+        const bool onR = lane != 63 && mr >= 0 && mr <= h && (uint32_t)(k >> mr) == xr;
+        const int m = onL ? ml : mr;
+        const uint64_t pulled = bperm64(av, (m + 1) & 63);
+        const int32_t pulledI = (int32_t)bperm32((uint32_t)avI, (m + 1) & 63);
+        const uint64_t nv = (m == h) ? val : pulled;
+        const int32_t nvI = (m == h) ? valI : pulledI;
+        if (onL) {
             L = nv;
-        if (writer && !takeL)
+            IL = nvI;
+        }
+        if (onR) {
             R = nv;
-        const uint64_t rootv = (W & 1ull) ? readlane64(chv, 0) : val;
-        if (!DRM_PQ_SROOT && lane == 63)
-            R = rootv;
-        return rootv;
-    }
-
-    // heap_push(128, val) right after pop128: val enters at slot 127 (lane 63 L); its ancestors are
-    // slots 63, 31, 15, 7, 3, 1 (the L halves of lanes 31, 15, 7, 3, 1, 0) and the root (lane 63 R).
-    // Every holder compares its own ancestor with val in place; chain index m = 7 - bitlen(lane + 1)
-    // receives its father's value (m < h) or val (m == h), fetched by one ds_bpermute.
-    // rootv: the root after the pop (pop128's return); returns the root after the push, wave-uniform
-    __device__ __forceinline__ uint64_t push128(uint64_t val, int lane, uint64_t rootv)
-    {
-        const bool holderL = lane == 63 || (lane < 32 && ((lane + 1) & lane) == 0); // slots 127, 63, ..., 1
-        // ancestors of slot 127: the L halves of lanes 0, 1, 3, 7, 15, 31 and lane 63 (its R is the root)
-        constexpr uint64_t kAnc = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
-#if DRM_PQ_SROOT
-        // the root is rootv (scalar); lane 63's R is stale until the hop refreshes it
-        constexpr uint64_t kAncL = kAnc & ~(1ull << 63);
-        const int h = __builtin_popcountll(ballot(val > L) & kAncL) + (val > rootv ? 1 : 0);
-#else
-        const uint64_t av = lane == 63 ? R : L;
-        const int h = __builtin_popcountll(ballot(val > av) & kAnc);
-#endif
-        const uint64_t fl = bperm64(L, lane >> 1);
-        const uint64_t srcv = lane == 0 ? rootv : fl;
-        const int m = 7 - bitlen((uint32_t)lane + 1u);
-        if (holderL && m <= h)
-            L = m < h ? srcv : val;
-        if (!DRM_PQ_SROOT && h == 7 && lane == 63)
+            IR = nvI;
+        }
+        // the root (lane 63 R, 1-based 1 = a_{bk-1}) changes only if val climbs all the way up
+        if (h == bk - 1 && lane == 63) {
             R = val;
-        return h == 7 ? val : rootv;
+            IR = valI;
+        }
     }
 
-#if DRM_PQ_HEAPV2
-    // pop128 with lane-mask predicates (DRM_PQ_HEAPV2): the same sift-down as pop128, with the path's lanes
-    // selected by their ballot masks (no per-lane mask arithmetic), and the last path node fetching the sifted
-    // value from lane 63 (slot 127 = val: lane 63 always takes its L) in the same ds_bpermute that moves the
-    // other children up. Lane 63's R (the root) is left stale (DRM_PQ_SROOT); returns the new root.
-    __device__ __forceinline__ uint64_t pop128v2(const PathConst &pc)
+    // heap_pop(128) then heap_push(128, vnew) on the full ef = 128 heap (MinimaxHeap::push when k == n), with the
+    // two cross-lane fetches issued together from the pre-pop registers: one ds_bpermute round trip per replace.
+    //  * pop: slot 127 (lane 63's L) is sifted down from the root. Lane p on the path writes its chosen child slot
+    //    with that child's own chosen child (chv of lane ch_p), or with slot 127's value when p is the path's last
+    //    node; the path is the set of lanes whose own and ancestors' chosen children move up (PathConst::path);
+    //  * push: vnew enters slot 127 and climbs the chain of its ancestors (slots 63, 31, 15, 7, 3, 1: the L halves
+    //    of lanes 31, 15, 7, 3, 1, 0; then the root). Chain holder c takes its father, slot c, whose post-pop value
+    //    is lane c's own chv (or slot 127's value) if lane c >> 1 is on the path and took its L child, else its
+    //    pre-pop value: the only cross-lane part is the pre-pop fetch.
+    // The root (slot 0) lives in scalar registers (root, rootI) during a row's pushes: lane 63's R key is left
+    // stale here and refreshed by the hop; returns the root after the push, its id in rootI.
+    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int lane,
+                                                   int32_t &rootI)
     {
-        const uint64_t val = readlane64(L, 63);
+        const uint64_t val = readlane64(L, 63); // slot 127
+        const int32_t valI = readlane32(IL, 63);
         const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child
         const bool takeL = in_mask(lm);
         const uint64_t chv = takeL ? L : R;
-        const uint64_t mv = ballot(!(val > chv));         // the chosen child moves up
-        const uint64_t W = pc.path(mv, lm);
-        if (!W)
-            return val; // the root's chosen child stays: val becomes the root
-        const uint32_t last = 63u - (uint32_t)__builtin_clzll(W);
-        uint32_t addr = takeL ? pc.addrL : pc.addrR;
-        addr = in_mask(1ull << last) ? (63u << 2) : addr;
-        const uint64_t up = bperm64_addr(chv, addr);
-        L = in_mask(W & lm) ? up : L;
-        R = in_mask(W & ~lm) ? up : R;
-        return (W & 1ull) ? readlane64(chv, 0) : val;
-    }
-
-    // push128 with lane-mask predicates: the chain holders below the insertion height take their fathers'
-    // values (one ds_bpermute from lane >> 1; slot 1 takes the root), the slot at the height takes val
-    __device__ __forceinline__ uint64_t push128v2(uint64_t val, const PathConst &pc, uint64_t rootv)
-    {
-        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
-        constexpr uint64_t kAncL = kHold & ~(1ull << 63); // slots 63, 31, 15, 7, 3, 1 (the root is rootv)
-        const int h = __builtin_popcountll(ballot(val > L) & kAncL) + (sgt64(val, rootv) ? 1 : 0);
-        const uint64_t fl = bperm64_addr(L, pc.addrHalf);
-        if (h == 0) { // val stays at slot 127
-            L = in_mask(1ull << 63) ? val : L;
-            return rootv;
-        }
-        // holders with chain index m = 7 - bitlen(lane + 1) < h: lanes >= 2^(7-h) - 1
-        const uint64_t mlt = kHold & (~0ull << ((1u << (7 - h)) - 1u));
-        L = in_mask(mlt) ? fl : L;
-        if (h == 7) { // val becomes the root; the old root moves down to slot 1 (lane 0)
-            L = in_mask(1ull) ? rootv : L;
-            return val;
-        }
-        L = in_mask(1ull << ((1u << (6 - h)) - 1u)) ? val : L; // the chain slot at index h
-        return rootv;
-    }
-
-    // pop128v2 then push128v2(vnew) with both cross-lane fetches issued together from the pre-pop registers
-    // (DRM_PQ_REPL1): one ds_bpermute round trip per full-heap replace instead of two in sequence.
-    //  * pop: lane p on the path writes its chosen child slot with that child's own chosen child (chv of lane ch_p),
-    //    or with slot 127's value when p is the path's last node; the fetch from lane ch_p needs no path knowledge,
-    //    so it leaves at once and the path (ballots, scalar masks) is formed while it is in flight;
-    //  * push: chain holder c (lanes 1, 3, 7, 15, 31, 63; slot 2c + 1 in its L) takes its father, slot c, held in
-    //    lane c >> 1's L. After the pop, slot c holds lane c's own chv (or slot 127's value) if lane c >> 1 is on the
-    //    path and took its L child, else its pre-pop value: the only cross-lane part is the pre-pop fetch.
-    // Same slots, same values as pop128v2 + push128v2; returns the root after the push.
-    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, const PathConst &pc, int lane)
-    {
-        const uint64_t val = readlane64(L, 63);            // slot 127
-        const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child
-        const bool takeL = in_mask(lm);
-        const uint64_t chv = takeL ? L : R;
-        const uint64_t up0 = bperm64_addr(chv, takeL ? pc.addrL : pc.addrR);
+        const int32_t chI = takeL ? IL : IR;
+        const uint32_t caddr = takeL ? pc.addrL : pc.addrR;
+        const uint64_t up0 = bperm64_addr(chv, caddr);
+        const int32_t up0I = bperm32_addr(chI, caddr);
         const uint64_t fpre = bperm64_addr(L, pc.addrHalf);
+        const int32_t fpreI = bperm32_addr(IL, pc.addrHalf);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
         uint64_t rootv = val;
+        int32_t rI = valI;
         uint32_t last = 64u;
         if (W) {
             last = 63u - (uint32_t)__builtin_clzll(W);
-            const uint64_t up = in_mask(1ull << last) ? val : up0;
-            L = in_mask(W & lm) ? up : L;
-            R = in_mask(W & ~lm) ? up : R;
-            rootv = (W & 1ull) ? readlane64(chv, 0) : val;
+            const bool atlast = in_mask(1ull << last);
+            const uint64_t up = atlast ? val : up0;
+            const int32_t upI = atlast ? valI : up0I;
+            const bool wl = in_mask(W & lm), wr = in_mask(W & ~lm);
+            L = wl ? up : L;
+            IL = wl ? upI : IL;
+            R = wr ? up : R;
+            IR = wr ? upI : IR;
+            if (W & 1ull) {
+                rootv = readlane64(chv, 0);
+                rI = readlane32(chI, 0);
+            }
         }
-        // heap_push(128, vnew): as push128v2, with the fathers' post-pop values formed locally
         constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         constexpr uint64_t kAncL = kHold & ~(1ull << 63);
         const int h = __builtin_popcountll(ballot(vnew > L) & kAncL) + (sgt64(vnew, rootv) ? 1 : 0);
         if (h == 0) {
-            L = in_mask(1ull << 63) ? vnew : L;
+            const bool s127 = in_mask(1ull << 63);
+            L = s127 ? vnew : L;
+            IL = s127 ? vnewI : IL;
+            rootI = rI;
             return rootv;
         }
         const uint32_t k = (uint32_t)lane >> 1;
         const bool moved = (((W & lm) >> k) & 1ull) != 0ull;
-        const uint64_t fl = moved ? (k == last ? val : chv) : fpre;
-        const uint64_t mlt = kHold & (~0ull << ((1u << (7 - h)) - 1u));
-        L = in_mask(mlt) ? fl : L;
-        if (h == 7) {
-            L = in_mask(1ull) ? rootv : L;
+        const bool klast = k == last;
+        const uint64_t fl = moved ? (klast ? val : chv) : fpre;
+        const int32_t flI = moved ? (klast ? valI : chI) : fpreI;
+        const bool wm = in_mask(kHold & (~0ull << ((1u << (7 - h)) - 1u))); // chain index < h
+        L = wm ? fl : L;
+        IL = wm ? flI : IL;
+        if (h == 7) { // vnew becomes the root; the old root moves down to slot 1 (lane 0)
+            const bool s1 = in_mask(1ull);
+            L = s1 ? rootv : L;
+            IL = s1 ? rI : IL;
+            rootI = vnewI;
             return vnew;
         }
-        L = in_mask(1ull << ((1u << (6 - h)) - 1u)) ? vnew : L;
+        const bool sx = in_mask(1ull << ((1u << (6 - h)) - 1u)); // the chain slot at index h
+        L = sx ? vnew : L;
+        IL = sx ? vnewI : IL;
+        rootI = rI;
         return rootv;
     }
 
@@ -405,9 +356,10 @@ struct Heap {
     // sifts up its ancestors, slot (k >> m) - 1 at chain index m (the root at m = bitlen(k) - 1). Lane-mask
     // form: each lane tests whether one of its halves is on the chain (both halves share the index), the
     // ancestors below val are a bottom prefix of length h (heap order), the slots of index < h take their
-    // father's value (two ds_bpermute per half), and the slot of index h takes val. The root is rootv (scalar;
-    // lane 63's R is left stale); returns the new root.
-    __device__ __forceinline__ uint64_t push_fill_v2(int k, uint64_t val, const PathConst &pc, uint64_t rootv)
+    // father's value (one ds_bpermute per half), and the slot of index h takes val. The root is (rootv, rootI)
+    // (scalar; lane 63's R key is left stale); returns the new root, its id in rootI.
+    __device__ __forceinline__ uint64_t push_fill(int k, uint64_t val, int32_t valI, const PathConst &pc, uint64_t rootv,
+                                                  int32_t &rootI)
     {
         const uint32_t s1 = (uint32_t)k;
         const int B = bitlen(s1);
@@ -420,54 +372,36 @@ struct Heap {
                       (sgt64(val, rootv) ? 1 : 0);
         if (h > 0) {
             const uint64_t fL = bperm64_addr(L, pc.addrF), fR = bperm64_addr(R, pc.addrF);
-            const uint64_t f = in_mask(0xAAAAAAAAAAAAAAAAull) ? fL : fR; // father slot p odd: an L half
-            const uint64_t mlt = ~0ull << ((1u << (B - h - 1)) - 1u);        // chain index < h: bl > B - h
-            L = in_mask(OL & mlt) ? f : L;
-            R = in_mask(OR & mlt) ? f : R;
+            const int32_t fLI = bperm32_addr(IL, pc.addrF), fRI = bperm32_addr(IR, pc.addrF);
+            const bool odd = in_mask(0xAAAAAAAAAAAAAAAAull); // father slot p odd: an L half
+            const uint64_t f = odd ? fL : fR;
+            const int32_t fI = odd ? fLI : fRI;
+            const uint64_t mlt = ~0ull << ((1u << (B - h - 1)) - 1u); // chain index < h: bl > B - h
+            const bool wl = in_mask(OL & mlt), wr = in_mask(OR & mlt);
+            L = wl ? f : L;
+            IL = wl ? fI : IL;
+            R = wr ? f : R;
+            IR = wr ? fI : IR;
             if (h == B - 1) { // val becomes the root; the old root moves to its child on the chain (lane 0)
-                L = in_mask(OL & 1ull) ? rootv : L;
-                R = in_mask(OR & 1ull) ? rootv : R;
+                const bool rl = in_mask(OL & 1ull), rr = in_mask(OR & 1ull);
+                L = rl ? rootv : L;
+                IL = rl ? rootI : IL;
+                R = rr ? rootv : R;
+                IR = rr ? rootI : IR;
+                rootI = valI;
                 return val;
             }
         }
         const uint32_t x = (s1 >> h) - 1u; // the slot of chain index h (>= 1 here)
-        const uint64_t xb = 1ull << ((x - 1u) >> 1);
-        if (x & 1u)
-            L = in_mask(xb) ? val : L;
-        else
-            R = in_mask(xb) ? val : R;
+        const bool xs = in_mask(1ull << ((x - 1u) >> 1));
+        if (x & 1u) {
+            L = xs ? val : L;
+            IL = xs ? valI : IL;
+        } else {
+            R = xs ? val : R;
+            IR = xs ? valI : IR;
+        }
         return rootv;
-    }
-#endif
-
-    // faiss heap_push<CMax<float, int>>(k, val): val enters at slot k-1 and sifts up (1-based k >= 1).
-    __device__ __forceinline__ void push(int k, uint64_t val, int lane)
-    {
-        // lane j in [1, 7] looks at the ancestor a_j = k >> j (1-based)
-        const int aj = (lane >= 1 && lane < 8) ? (k >> lane) : 0;
-        const int t = aj - 1; // its slot
-        const int owner = t <= 0 ? 63 : (t - 1) >> 1;
-        const bool sideR = t <= 0 || !(t & 1);
-        const uint64_t fl = bperm64(L, owner), fr = bperm64(R, owner);
-        const uint64_t av = sideR ? fr : fl;
-        const bool moves = aj >= 1 && val > av; // cmp2(val, father): the father moves down
-        const int h = __builtin_popcountll(ballot(moves)); // ancestors 1..h move (heap order: a prefix)
-        // chain index m (a_m = k >> m, m = 0..h) gets a_{m+1}'s value, or val at m == h
-        const int bk = bitlen((uint32_t)k);
-        const uint32_t xl = 2u * (uint32_t)lane + 2u, xr = xl + 1u; // 1-based indices of L, R
-        const int ml = bk - bitlen(xl), mr = bk - bitlen(xr);
-        const bool onL = ml >= 0 && ml <= h && (uint32_t)(k >> ml) == xl;
-        const bool onR = lane != 63 && mr >= 0 && mr <= h && (uint32_t)(k >> mr) == xr;
-        const int m = onL ? ml : mr;
-        const uint64_t pulled = bperm64(av, (m + 1) & 63);
-        const uint64_t nv = (m == h) ? val : pulled;
-        if (onL)
-            L = nv;
-        if (onR)
-            R = nv;
-        // the root (lane 63 R, 1-based 1 = a_{bk-1}) changes only if val climbs all the way up
-        if (h == bk - 1 && lane == 63)
-            R = val;
     }
 };
 
@@ -497,23 +431,10 @@ __device__ __forceinline__ void sort128(uint64_t &x0, uint64_t &x1, int lane)
     }
 }
 
-// Link `lane` of an inline level-0 row (DeviceIndex::rows): its id and its 8-byte PQ code, interleaved as 12 bytes
-// per link, so the whole row (32 links = 384 B at M_hnsw = 16) is one dwordx3 load of the wave instead of an id load
-// and a code load: every VMEM instruction a hop issues costs the CU's memory pipeline the same ~80-150 cycles
-// whatever the footprint (tools/microbench/vispattern.hip). Lanes past deg0 get (-1, 0).
-__device__ __forceinline__ void load_link(const int32_t *row, int lane, int deg0, int32_t &id, uint2 &code)
-{
-    id = -1;
-    code = make_uint2(0u, 0u);
-    if (lane < deg0) {
-        const int32_t *e = row + 3 * lane;
-        id = e[0];
-        code = make_uint2((uint32_t)e[1], (uint32_t)e[2]);
-    }
-}
-
-// The raw 12 bytes of link j of an inline row, loaded by every lane (lanes past deg0 read link 0 and are masked at
-// the use): no branch around the load, so the compiler can count it and leave it in flight (DRM_PQ_ASYNC).
+// The raw 12 bytes (id, 8-byte PQ code) of link `lane` of an inline level-0 row (DeviceIndex::rows), loaded by
+// every lane (lanes past deg0 read link 0 and are masked at the use): the whole row (32 links = 384 B at
+// M_hnsw = 16) is one dwordx3 load of the wave, with no branch around it, so the compiler can count it and leave
+// it in flight until the next hop.
 struct __attribute__((aligned(4))) Link3 {
     uint32_t x, y, z;
 };
@@ -626,27 +547,6 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     return cnt;
 }
 
-#ifndef DRM_PQ_VIS_LOAD
-#define DRM_PQ_VIS_LOAD 1 // inline kernel: visited test by an L2 load, fresh links marked afterwards (0: test-and-set)
-#endif
-
-#ifndef DRM_PQ_LOGSTAGE
-// k == ef: accepted pushes are staged in a 64-entry register buffer (lane sn takes the push loop's scalars) and stored to the slot's log 64 at a time, instead of one store instruction per hop (0: per-hop store)
-#define DRM_PQ_LOGSTAGE 1
-#endif
-
-#ifndef DRM_PQ_ASYNC
-// inline kernel: the predicted next row is loaded by an unconditional instruction and only waited for at the next
-// hop, and the visited test is an unconditional load, so a hop waits for its visited answer alone (vmcnt counts the
-// row load still in flight). 0: the row load sits in a branch, and the compiler waited for it right away (the copy
-// into the loop-carried registers), i.e. after the ADC and the prediction, on the hop's critical path.
-#define DRM_PQ_ASYNC 1
-#endif
-
-#ifndef DRM_PQ_SPEC
-#define DRM_PQ_SPEC 0 // codes + visited words of the predicted next row loaded one hop ahead (measured slower)
-#endif
-
 #define DRM_FSTAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -659,14 +559,13 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     } while (0)
 
 // LOGRES: k == ef (result set from the log); else k <= 64 (register result set).
-// FIX128: ef = efSearch = 128 (and k = 128 with LOGRES) and no repeated links as compile-time constants:
-// the pipeline's EF = K = 128 on a clean index, and the sparse default k_clusters = 5 at EF = 128
-// (src/main.cpp:56-63,278) -- fewer live SGPRs (no spills to VGPR lanes, no kernel-argument reloads
-// inside the hop loop) and no duplicate-link pass.
-// INL: the level-0 rows carry their neighbours' PQ codes (SearchArgs::rows): one row fetch gives a hop its
-// distances, the next row is predicted and prefetched from them while the visited-bitmap test is in flight,
-// and only that test's round trip stays on the hop's critical path.
-template <bool LOGRES, bool STAMPS, bool FIX128, bool INL = false>
+// FIX128: ef = efSearch = 128 (and k = 128 with LOGRES) as compile-time constants: the pipeline's EF = K = 128,
+// and the sparse default k_clusters = 5 at EF = 128 (src/main.cpp:56-63,278) -- fewer live SGPRs.
+// STATS: faiss's HNSWStats.ndis (links never seen before) counted exactly with a per-slot bitmap beside the heap
+// (SearchArgs::visited, cleared from a list after each query). Nothing else depends on it; without it ndis counts
+// the distances the kernel computed (every valid link of every expanded row, plus the upper levels).
+// STAMPS: diagnostic section timers (DRM_SEARCH_STAMPS=1).
+template <bool LOGRES, bool STAMPS, bool FIX128, bool STATS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hnsw_pq_fast_kernel(SearchArgs a)
 {
     // the 8 x 256 f32 LUT (the kernel's only LDS): a static allocation at LDS address 0, so the LUT reads
@@ -677,17 +576,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
     uint64_t *stage = reinterpret_cast<uint64_t *>(smem); // reuses the LUT once the walk is over
-    uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
-    int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
+    uint32_t *vis = STATS ? a.visited + (size_t)blockIdx.x * (size_t)a.vis_words : nullptr;
+    int32_t *clr = STATS ? a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap : nullptr;
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
     const int ef = FIX128 ? 128 : a.ef, k = (FIX128 && LOGRES) ? 128 : a.k, deg0 = a.deg0;
     const int ef_search = FIX128 ? 128 : a.efSearch;
-    const bool check_dups = FIX128 ? false : (a.check_dups != 0);
     const PathConst pconst(lane);
-    const uint64_t deg0m = deg0 >= 64 ? ~0ull : ((1ull << deg0) - 1ull); // lanes holding a link slot
     const uint32_t kInfKey = ord32(INFINITY);
-    // INL: this slot's query generation (the tag of its visited words), carried across launches
-    uint32_t gen = INL ? a.vis_gen[blockIdx.x] : 0u;
 
     for (;;) {
         int q = 0;
@@ -696,15 +591,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         q = __builtin_amdgcn_readfirstlane(q);
         if ((int64_t)q >= a.n)
             break;
-        if (INL) { // a new generation per query; at the 16-bit wrap the slot's words restart from zero
-            gen += 1u;
-            if (gen > 0xFFFFu) {
-                uint4 *v4 = reinterpret_cast<uint4 *>(vis);
-                for (int64_t w = lane; w < a.vis_words / 4; w += 64)
-                    v4[w] = make_uint4(0u, 0u, 0u, 0u);
-                gen = 1u;
-            }
-        }
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < k; j += 64) {
                 a.D[(int64_t)q * k + j] = INFINITY;
@@ -727,7 +613,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         int32_t nearest;
         uint32_t dn;
         int ndis, nhops;
-        if (INL && a.upper_codes)
+        if (a.upper_codes)
             greedy_upper_inl(a, lut, lane, nearest, dn, ndis, nhops);
         else
             greedy_upper<true>(a, lut, lane, nearest, dn, ndis, nhops);
@@ -738,8 +624,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         Heap hp;
         hp.L = kUnused;
         hp.R = lane == 63 ? pack(dn, nearest) : kUnused;
+        hp.IL = -1;
+        hp.IR = lane == 63 ? nearest : -1;
         int kc = 1, nvalid = 1;
         uint64_t root = pack(dn, nearest); // slot 0
+        int32_t rootI = nearest;
         // result set: the log (LOGRES) or a sorted register set of k <= 64 entries
         int logn = 0;
         uint64_t rv = ~0ull; // !LOGRES: lane j < k holds the j-th smallest (key, id) so far
@@ -750,7 +639,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             rv = lane > pos ? sh : (lane == pos ? v : rv);
             thr = (uint32_t)__builtin_amdgcn_readlane((int)hi32(rv), k - 1);
         };
-        // DRM_PQ_LOGSTAGE: accepted pushes not yet stored, lanes [0, sn) of (sbh, sbl) = (key, id ^ 2^31) in log order
+        // accepted pushes not yet stored (k == ef): lanes [0, sn) of (sbh, sbl) = (key, id ^ 2^31) in log order
         uint32_t sbh = 0u, sbl = 0u;
         int sn = 0;
         // compacts the stored log to the current k results when the staged entries would overflow it (T = the heap
@@ -779,35 +668,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (dn < thr)
                 add_result(root);
         }
-        if (lane == 0) {
-            if (INL) // the query's first mark: the word's generation is an older one
-                __hip_atomic_store(&vis[nearest >> 4], (gen << 16) | (1u << (nearest & 15)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-                vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
-            if (!INL && a.clear_cap > 0)
+        int clear_n = 1;
+        if (STATS && lane == 0) { // vt.set(entry)
+            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
+            if (a.clear_cap > 0)
                 clr[0] = nearest;
         }
-        int clear_n = 1;
         int nstep = 0, ndis0 = 0;
-        int32_t pred = -1, v1_pref = -1;
-        // one hop ahead (DRM_PQ_SPEC): the codes of the predicted row's links and their visited-bitmap
-        // words, loaded with plain L2 loads at the end of the previous hop. Exact: only this wave marks
-        // its bitmap, its marks of that hop were issued before the predicted row's load (VMEM completes
-        // in order and these loads depend on that row), and nothing marks between here and their use.
-        bool spec = false;
-        uint2 c8_pref = make_uint2(0u, 0u);
-        uint32_t vw_pref = 0u;
-        // INL: a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row
-        // prediction can skip links back to nodes already expanded before the visited test has answered
+        bool overrun = false;
+        int32_t pred = -1;
+        // a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row prediction can
+        // skip links back to nodes already expanded
         uint32_t popped_bits = 0u;
-        // DRM_PQ_TAGMARK == 4: the previous hop's restart marks -- lanes that issued one, the value each found, its id
-        uint64_t mstale = 0;
-        uint32_t mret = 0u;
-        int32_t mprev = -1;
-        Link3 praw{0xFFFFFFFFu, 0u, 0u}; // DRM_PQ_ASYNC: the predicted row's link `lane`, raw (pred = -1: none yet)
+        Link3 praw{0xFFFFFFFFu, 0u, 0u}; // the predicted row's link `lane`, raw (pred = -1: none yet)
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
         while (nvalid > 0) {
+            // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
+            // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the
+            // bookkeeping is broken -- end the query with an error status rather than loop
+            if (nstep > a.ntotal) {
+                overrun = true;
+                break;
+            }
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
@@ -840,70 +722,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 break;
             DRM_FSTAMP(2);
 
-            int32_t v1;
-            uint32_t dk;
-            uint64_t fm;
-            // expand v0's level-0 row (one coalesced load, lane j = link j)
-            v1 = v1_pref;
+            // expand v0's level-0 row: its ids and codes arrive with one load, prefetched one hop ago when the
+            // prediction held
             const bool hit = v0 == pred;
             if (STAMPS) { // row prediction hits / hops
                 st_acc[8] += hit ? 1u : 0u;
                 st_acc[9] += 1u;
             }
-            if (INL) {
+            {
                 const uint32_t h0 = pop_hash(v0);
                 if (lane == (int)((h0 >> 5) & 63u))
                     popped_bits |= 1u << (h0 & 31u);
-                if (DRM_PQ_ASYNC) {
-                    if (!hit)
-                        praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
-                    v1 = lane < deg0 ? (int32_t)praw.x : -1;
-                    c8_pref = lane < deg0 ? make_uint2(praw.y, praw.z) : make_uint2(0u, 0u);
-                    if (STAMPS) { // the row is in registers (its wait covers the previous hop's marks)
-                        const uint32_t tch = __builtin_amdgcn_readfirstlane((uint32_t)v1 ^ c8_pref.x);
-                        st_acc[10] += tch == 0x5A5A5A5Au ? 1u : 0u;
-                        DRM_FSTAMP(10);
-                    }
-                } else if (!hit)
-                    load_link(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0, v1, c8_pref);
-            } else if (!hit)
-                v1 = lane < deg0 ? a.nbr0[(size_t)v0 * (size_t)deg0 + lane] : -1;
-            const uint64_t negm = ballot(v1 < 0) & deg0m;
-            const int jmax = negm ? __builtin_ctzll(negm) : deg0;
-            const bool act = lane < jmax;
-            const uint64_t actm = jmax >= 64 ? ~0ull : ((1ull << jmax) - 1ull);
-            uint2 c8 = make_uint2(0u, 0u);
-            uint32_t old = 0xFFFFFFFFu;
-            // INL: tagged words (16 node bits | generation << 16); else the plain bitmap (32 node bits)
-            const uint32_t bit = INL ? 1u << (v1 & 15) : 1u << (v1 & 31);
-            const bool use_spec = !INL && DRM_PQ_SPEC && hit && spec;
-            if (INL) {
-                c8 = c8_pref; // arrived with the row
-                // the visited test is in flight while the distances are formed: a plain L2 load (sc1: this wave's
-                // own earlier marks are at L2, never in its L1), and only the fresh links are marked afterwards.
-                // Exact: this wave alone writes its words, its earlier marks were issued before this load, and a
-                // repeated id in one row is fresh once (check_dups below) and so marked once.
-                if (DRM_PQ_ASYNC) // every lane loads (the inactive ones word 0), no branch
-                    old = __hip_atomic_load(&vis[act ? (v1 >> 4) : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else if (act)
-                    old = __hip_atomic_load(&vis[v1 >> 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else if (use_spec) {
-                c8 = c8_pref;
-                old = act ? vw_pref : 0xFFFFFFFFu;
-            } else if (act) {
-                c8 = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1 * 8); // overlaps the visited test
-                old = vis_test_set(&vis[v1 >> 5], bit);
             }
-            uint32_t dall = 0xFFFFFFFFu;
-            if (INL) {
-                // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min:
-                // the smallest valid heap slot or active link not known to be popped; its row (ids + codes) is
-                // fetched now, beside the visited test
-                dall = adc8(lut, c8);
+            if (!hit)
+                praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
+            const int32_t v1 = lane < deg0 ? (int32_t)praw.x : -1;
+            const uint2 c8 = lane < deg0 ? make_uint2(praw.y, praw.z) : make_uint2(0u, 0u);
+            const uint64_t negm = ballot(v1 < 0);
+            const int jmax = negm ? __builtin_ctzll(negm) : 64; // lanes past deg0 hold -1
+            const uint64_t actm = negm ? (negm & (0ull - negm)) - 1ull : ~0ull;
+            DRM_FSTAMP(10);
+            // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min: the
+            // smallest valid heap slot or link not known to be popped; its row is fetched now and waited for at
+            // the next hop
+            const uint32_t dall = adc8(lut, c8);
+            {
                 const uint32_t hv = pop_hash(v1);
                 const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
                 const bool known_popped = (pw >> (hv & 31u)) & 1u;
-                const uint32_t dp = (act && !known_popped) ? dall : 0xFFFFFFFFu;
+                const uint32_t dp = (lane < jmax && !known_popped) ? dall : 0xFFFFFFFFu;
                 const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
                 const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
                 uint32_t mk = dp < hL ? dp : hL;
@@ -911,220 +758,82 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const int32_t mid = dp == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
                 const uint32_t mm = wave_min_u32(mk);
                 pred = -1;
-                if (DRM_PQ_ASYNC) {
-                    // no prediction (the heap and the row hold nothing valid): load v0's row again, pred stays -1
-                    int32_t pnode = v0;
-                    if (mm != 0xFFFFFFFFu) {
-                        pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
-                        pnode = pred;
-                    }
-                    praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
-                } else if (mm != 0xFFFFFFFFu) {
-                    pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
-                    load_link(a.rows + (size_t)pred * (size_t)a.row_words, lane, deg0, v1_pref, c8_pref);
-                }
-            }
-            // visited in this query: (tagged) the word carries this query's generation and the node's bit
-            bool seen = INL ? ((old >> 16) == gen && (old & bit) != 0u) : (old & bit) != 0u;
-#if DRM_PQ_TAGMARK == 4
-            // the previous hop's restart marks (one returning atomic max per fresh link on a stale word): a link that
-            // found its word already restarted in that same instruction (a "follower": another fresh link of the row
-            // shares the word) may have lost its bit in the max, or dropped the bits it found -- it now ORs back the
-            // word it saw plus its own bit, so every bit of the group ends up set. This row's visited load was issued
-            // before that repair, so a link whose word is a follower's and whose bit is in what the follower saw or
-            // its own bit counts as visited (any such bit is this query's). Followers are rare: the branch is
-            // usually not taken.
-            if (INL && mstale) {
-                const uint64_t F = ballot(((mstale >> lane) & 1ull) && (mret >> 16) == gen);
-                if (F) {
-                    const uint32_t fix = mret | (gen << 16) | (1u << (mprev & 15));
-                    if ((F >> lane) & 1ull)
-                        __hip_atomic_fetch_or(&vis[mprev >> 4], fix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    for (uint64_t f = F; f; f &= f - 1) {
-                        const int fl = __builtin_ctzll(f);
-                        const int32_t fw = __builtin_amdgcn_readlane(mprev, fl) >> 4;
-                        const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)fix, fl);
-                        seen = seen || (act && (v1 >> 4) == fw && ((fb >> (v1 & 15)) & 1u) != 0u);
-                    }
-                }
-            }
-#endif
-            bool fresh = act && !seen;
-#if DRM_PQ_TAGMARK == 5
-            bool mshared = false; // two fresh links of this row on one stale word (decided after check_dups below)
-#endif
-            if (check_dups) { // a repeated id in one row: only its first occurrence is fresh
-                for (int j = 0; j < jmax; ++j) {
-                    const int32_t vj = __shfl(v1, j, 64);
-                    if (j < lane && vj == v1)
-                        fresh = false;
-                }
-            }
-#if DRM_PQ_TAGMARK == 5
-            if (INL) {
-                const uint64_t S = ballot(fresh && (old >> 16) != gen);
-                const uint32_t wv = (uint32_t)v1 >> 4;
-                for (uint64_t rest = S; rest;) {
-                    const uint32_t wl = (uint32_t)__builtin_amdgcn_readlane((int)wv, __builtin_ctzll(rest));
-                    const uint64_t same = ballot(wv == wl) & S;
-                    if (same & (same - 1)) {
-                        mshared = true;
-                        break;
-                    }
-                    rest &= ~same;
-                }
-            }
-#endif
-            if (INL && fresh) {
-                // mark the fresh links: a word still carrying an older generation is restarted with this one
-                // (atomic max with gen << 16: generations only grow between wraps, so the max drops the old tag
-                // and bits), then every fresh link ORs in its bit; both atomics of a lane go to one address in
-                // order, and lanes sharing a word all OR their bits after it restarted, so no bit is lost
-                const uint32_t tagbit = (gen << 16) | bit;
-#if DRM_PQ_TAGMARK == 0
-                if ((old >> 16) != gen)
-                    __hip_atomic_store(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#elif DRM_PQ_TAGMARK == 1
-                if ((old >> 16) != gen)
-                    __hip_atomic_fetch_max(&vis[v1 >> 4], gen << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-#if DRM_PQ_TAGMARK == 3
-                // timing diagnostic only (inexact when two fresh links of a row share a stale word): one atomic per link
-                if ((old >> 16) != gen)
-                    __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#elif DRM_PQ_TAGMARK == 5
-                // one atomic per fresh link unless two fresh links of this row share a stale word (checked exactly
-                // over the stale words below, wave-uniform): then the two-atomic form for the row
-                if (!mshared) {
-                    if ((old >> 16) != gen)
-                        __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    else
-                        __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    if ((old >> 16) != gen)
-                        __hip_atomic_fetch_max(&vis[v1 >> 4], gen << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-#elif DRM_PQ_TAGMARK == 4
-                // one atomic per fresh link: a stale word is restarted with this link's bit by an atomic max (the first
-                // lane of the instruction to reach the word wins; the returned value tells the others, repaired at
-                // the next hop); a word of this generation takes the bit by an OR
-                if ((old >> 16) != gen)
-                    mret = __hip_atomic_fetch_max(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-                __hip_atomic_fetch_or(&vis[v1 >> 4], tagbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-            } else if (use_spec && fresh) // the test was a load: mark the fresh links
-                __hip_atomic_fetch_or(&vis[v1 >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if DRM_PQ_TAGMARK == 4
-            if (INL) {
-                mstale = ballot(fresh && (old >> 16) != gen);
-                mprev = v1;
-            }
-#endif
-            DRM_FSTAMP(3);
-            fm = check_dups ? ballot(fresh) : ballot(!seen) & actm;
-            const int nf = __builtin_popcountll(fm);
-            ndis0 += nf;
-            // PQ-ADC distance, sequential over the 8 sub-quantizers (computed on every lane, kept
-            // on the fresh ones)
-            // all 8 LDS reads in flight before the first add (the adds stay in sub-quantizer order)
-            if (INL) {
-                dk = fresh ? dall : 0xFFFFFFFFu;
-            } else {
-            float lv[8];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                lv[m] = lut[m * 256 + ((c8.x >> (8 * m)) & 255u)];
-                lv[m + 4] = lut[(m + 4) * 256 + ((c8.y >> (8 * m)) & 255u)];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            float r = 0.0f;
-#pragma unroll
-            for (int m = 0; m < 8; ++m)
-                r = __fadd_rn(r, lv[m]);
-            dk = fresh ? ord32(r) : 0xFFFFFFFFu;
-            }
-            if (!INL) {
-                // prefetch the row of the likely next pop_min (smallest valid slot or fresh link)
-                const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
-                const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
-                uint32_t mk = dk < hL ? dk : hL;
-                mk = mk < hR ? mk : hR;
-                const int32_t mid = dk == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
-                const uint32_t mm = wave_min_u32(mk);
-                pred = -1;
+                // no prediction (the heap and the row hold nothing valid): load v0's row again, pred stays -1
+                int32_t pnode = v0;
                 if (mm != 0xFFFFFFFFu) {
                     pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
-                    v1_pref = lane < deg0 ? a.nbr0[(size_t)pred * (size_t)deg0 + lane] : -1;
+                    pnode = pred;
                 }
+                praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
             }
-            if (!INL && fresh) { // VisitedTable::advance list (stored after the loads above)
-                const int p = clear_n + __builtin_popcountll(fm & lanes_below(lane));
-                if (p < a.clear_cap)
-                    clr[p] = v1;
+            if (STATS) {
+                // VisitedTable get + set of every link, in row order (lanes of one atomic instruction that share a
+                // word are serialised: exactly one finds a repeated id fresh); the count is all it feeds
+                const bool act = lane < jmax;
+                const uint32_t bit = 1u << (v1 & 31);
+                const uint32_t old = act ? vis_test_set(&vis[v1 >> 5], bit) : 0xFFFFFFFFu;
+                const bool fresh = act && !(old & bit);
+                const uint64_t fm = ballot(fresh);
+                if (fresh) { // VisitedTable::advance list
+                    const int p = clear_n + __builtin_popcountll(fm & lanes_below(lane));
+                    if (p < a.clear_cap)
+                        clr[p] = v1;
+                }
+                clear_n += __builtin_popcountll(fm);
+                ndis0 += __builtin_popcountll(fm);
+            } else {
+                ndis0 += jmax;
             }
-            clear_n += nf;
-            DRM_FSTAMP(4);
-            // add_to_heap for each fresh link in row order. On a full heap the root distance only
-            // falls, so a link at or above it now is rejected for the whole row: it is skipped here. It cannot
-            // enter a k < ef result set either: the heap keeps the ef smallest pushed keys (popped slots keep
-            // theirs), so its root is at or above the k-th smallest result, the threshold add_result tests.
-            uint64_t rem = fm, accm = 0;
-            bool replaced = false;
+            DRM_FSTAMP(3);
+            // add_to_heap for each link not seen before, in row order. On a full heap a link at or above the root is
+            // rejected now and on any later encounter (the root only falls): skipped whether seen or not. A link
+            // below the root was seen iff it is in the heap (popped or not): a seen link either entered the heap
+            // and is still there, or was rejected / evicted at a root that is now at or below its distance.
+            uint64_t rem = actm;
             if (kc == ef)
-                rem &= ballot(dk < hi32(root));
+                rem &= ballot(dall < hi32(root));
+            bool replaced = false;
             while (rem) {
                 const int l = __builtin_ctzll(rem);
                 rem &= rem - 1;
-                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
+                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
+                if (kc == ef && key >= hi32(root))
+                    continue;
+                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                if (hp.holds(idl))
+                    continue;
+                const uint64_t val = pack(key, idl);
                 if (!LOGRES) {
                     if (key < thr)
-                        add_result(pack(key, __builtin_amdgcn_readlane(v1, l)));
+                        add_result(val);
                 }
-                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
-                const uint64_t val = pack(key, idl);
                 if (kc == ef) { // MinimaxHeap::push on a full heap: pop the max, push val
-                    if (key >= hi32(root))
-                        continue;
                     if (lo32(root) != kPopLo)
                         --nvalid;
                     if (ef == 128) {
-#if DRM_PQ_HEAPV2 && DRM_PQ_REPL1
-                        root = hp.replace128(val, pconst, lane);
-#elif DRM_PQ_HEAPV2
-                        root = hp.push128v2(val, pconst, hp.pop128v2(pconst));
-#else
-                        root = hp.push128(val, lane, hp.pop128(lane, pconst));
-#endif
+                        root = hp.replace128(val, idl, pconst, lane, rootI);
+                        hp.IR = in_mask(1ull << 63) ? rootI : hp.IR;
                         replaced = true;
                         if (STAMPS)
                             st_acc[11] += 1u;
                     } else {
                         hp.pop(kc, lane);
-                        hp.push(kc, val, lane);
+                        hp.push(kc, val, idl, lane);
                         root = readlane64(hp.R, 63);
                     }
                 } else {
                     ++kc;
-#if DRM_PQ_HEAPV2
                     if (ef == 128) {
-                        root = hp.push_fill_v2(kc, val, pconst, root);
+                        root = hp.push_fill(kc, val, idl, pconst, root, rootI);
+                        hp.IR = in_mask(1ull << 63) ? rootI : hp.IR;
                         replaced = true;
-                    } else
-#endif
-                    {
-                        hp.push(kc, val, lane);
+                    } else {
+                        hp.push(kc, val, idl, lane);
                         root = readlane64(hp.R, 63);
                     }
                 }
                 ++nvalid;
-                accm |= 1ull << l;
-                if (LOGRES && DRM_PQ_LOGSTAGE) {
+                if (LOGRES) {
                     if (sn == 64)
                         log_flush();
                     const bool at = lane == sn; // lane sn takes the entry (one compare, two selects)
@@ -1133,42 +842,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     ++sn;
                 }
             }
-            if (DRM_PQ_SROOT && replaced && lane == 63)
+            if (replaced && lane == 63) // the ef = 128 pushes kept the root in scalars
                 hp.R = root;
-            if (LOGRES && !DRM_PQ_LOGSTAGE && accm) {
-                const int na = __builtin_popcountll(accm);
-                if (logn + na > a.log_cap) {
-                    // compact in place: the current result set (k entries) replaces the log
-                    const uint32_t T = hi32(root);
-                    const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
-                    logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
-                        __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }, lane);
-                    __builtin_amdgcn_s_waitcnt(0);
-                }
-                if ((accm >> lane) & 1ull)
-                    __hip_atomic_store(lg + logn + __builtin_popcountll(accm & lanes_below(lane)), pack(dk, v1),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                logn += na;
-            }
             nstep++;
-            spec = false;
-            if (!INL && DRM_PQ_SPEC && pred >= 0) {
-                const uint64_t pneg = ballot(lane < deg0 && v1_pref < 0);
-                const int pmax = pneg ? __builtin_ctzll(pneg) : deg0;
-                if (lane < pmax) {
-                    c8_pref = *reinterpret_cast<const uint2 *>(a.codes + (size_t)v1_pref * 8);
-                    vw_pref = __hip_atomic_load(&vis[v1_pref >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // L2, not L1
-                }
-                spec = true;
-            }
             DRM_FSTAMP(5);
         }
         DRM_FSTAMP(2);
 
         // --- SingleResultHandler::end (heap_reorder): ascending (distance, id), (+inf, -1) padding
         if (LOGRES) {
-            if (DRM_PQ_LOGSTAGE && sn)
+            if (sn)
                 log_flush();
             __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
             __syncthreads();
@@ -1199,29 +882,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             a.I[o] = valid ? (int64_t)unpack_id(rv) : (int64_t)-1;
         }
         if (lane == 0) {
-            a.ndis[q] = ndis + ndis0;
-            a.nhops[q] = nhops + nstep;
+            a.ndis[q] = overrun ? -1 : ndis + ndis0;
+            a.nhops[q] = overrun ? -1 : nhops + nstep;
             if (a.nhops_upper)
                 a.nhops_upper[q] = nhops_upper;
+            if (overrun)
+                atomicAdd(a.counter + 3, 1u);
         }
-        // VisitedTable::advance: clear exactly the bits this query set (INL: nothing to clear, the next query
-        // has a new generation)
-        if (INL) {
-        } else if (clear_n <= a.clear_cap) {
-            for (int t = lane; t < clear_n; t += 64)
-                vis[clr[t] >> 5] = 0u;
-        } else {
-            for (int64_t w = lane; w < a.vis_words; w += 64)
-                vis[w] = 0u;
-        }
-        if (!INL) { // the clears land before the next query's tests
+        if (STATS) { // VisitedTable::advance: clear exactly the bits this query set; they land before the next query
+            if (clear_n <= a.clear_cap) {
+                for (int t = lane; t < clear_n; t += 64)
+                    vis[clr[t] >> 5] = 0u;
+            } else {
+                for (int64_t w = lane; w < a.vis_words; w += 64)
+                    vis[w] = 0u;
+            }
             __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
         }
         DRM_FSTAMP(6);
     }
-    if (INL && lane == 0)
-        a.vis_gen[blockIdx.x] = gen;
     if (STAMPS && lane == 0 && a.stamps)
         for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
@@ -1289,43 +969,37 @@ void build_inline_rows(DeviceIndex &ix)
 
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 {
-    return ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8 && ix.deg0 <= 64 && efc <= 128 &&
-           (k == efc || k <= 64) && ix.vmode == 0;
+    return ix.rows != nullptr && ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8 && ix.deg0 <= 64 &&
+           efc <= 128 && (k == efc || k <= 64) && ix.vmode == 0;
 }
 
-void launch_hnsw_pq_fast(const SearchArgs &a, int slots, size_t lds, bool stamps, hipStream_t stream)
+void launch_hnsw_pq_fast(const SearchArgs &a, int slots, bool stamps, hipStream_t stream)
 {
-    (void)lds; // static LDS (the LUT)
     const bool logres = a.k == a.ef;
-    const bool fix = a.ef == 128 && a.efSearch == 128 && !a.check_dups && !stamps;
-    const bool inl = a.rows != nullptr;
-    if (stamps && inl && logres && a.ef == 128 && a.efSearch == 128 && !a.check_dups)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, true, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (fix && logres && inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (fix && inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (inl && logres && stamps)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (inl && logres)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (inl)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (fix && logres)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, true>), dim3(slots), dim3(64), 0, stream, a);
+    const bool fix = a.ef == 128 && a.efSearch == 128;
+    const bool stats = a.exact_stats != 0;
+#define DRM_LAUNCH_FAST(LR, ST, FX, XS)                                                                          \
+    hipLaunchKernelGGL((hnsw_pq_fast_kernel<LR, ST, FX, XS>), dim3(slots), dim3(64), 0, stream, a)
+    if (stamps && logres && fix && !stats)
+        DRM_LAUNCH_FAST(true, true, true, false);
+    else if (stats) {
+        if (fix && logres)
+            DRM_LAUNCH_FAST(true, false, true, true);
+        else if (fix)
+            DRM_LAUNCH_FAST(false, false, true, true);
+        else if (logres)
+            DRM_LAUNCH_FAST(true, false, false, true);
+        else
+            DRM_LAUNCH_FAST(false, false, false, true);
+    } else if (fix && logres)
+        DRM_LAUNCH_FAST(true, false, true, false);
     else if (fix)
-        hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, true>), dim3(slots), dim3(64), 0, stream, a);
-    else if (logres) {
-        if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, true, false>), dim3(slots), dim3(64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<true, false, false>), dim3(slots), dim3(64), 0, stream, a);
-    } else {
-        if (stamps)
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, true, false>), dim3(slots), dim3(64), 0, stream, a);
-        else
-            hipLaunchKernelGGL((hnsw_pq_fast_kernel<false, false, false>), dim3(slots), dim3(64), 0, stream, a);
-    }
+        DRM_LAUNCH_FAST(false, false, true, false);
+    else if (logres)
+        DRM_LAUNCH_FAST(true, false, false, false);
+    else
+        DRM_LAUNCH_FAST(false, false, false, false);
+#undef DRM_LAUNCH_FAST
     DRM_HIP_CHECK(hipGetLastError());
 }
 

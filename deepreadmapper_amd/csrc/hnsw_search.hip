@@ -1011,28 +1011,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
 } // namespace
 
 // Per-slot search workspace (visited bitmaps, clear lists, queue counters, the lean kernel's push log)
-// for a full-occupancy grid, allocated once at index load so that no search pays for it (at C5 the
-// bitmaps alone are 32 GB). Searches that need more (other LUT sizes, larger logs) still grow it.
-// The inline-row lean kernel's tagged visited words for `slots` slots (zeroed: generation 0 is never a query's)
-static void ensure_tagged(DeviceIndex &ix, int slots)
-{
-    const int64_t words = ((ix.ntotal + 15) / 16 + 3) / 4 * 4;
-    if (ix.vis_tag && ix.tag_slots >= slots && ix.tag_words == words)
-        return;
-    if (ix.vis_tag)
-        DRM_HIP_CHECK(hipFree(ix.vis_tag));
-    if (ix.vis_gen)
-        DRM_HIP_CHECK(hipFree(ix.vis_gen));
-    ix.vis_tag = nullptr;
-    ix.vis_gen = nullptr;
-    DRM_HIP_CHECK(malloc_big((void **)&ix.vis_tag, sizeof(uint32_t) * (size_t)slots * (size_t)words, kBigVisited));
-    DRM_HIP_CHECK(hipMemset(ix.vis_tag, 0, sizeof(uint32_t) * (size_t)slots * (size_t)words));
-    DRM_HIP_CHECK(hipMalloc(&ix.vis_gen, sizeof(uint32_t) * (size_t)slots));
-    DRM_HIP_CHECK(hipMemset(ix.vis_gen, 0, sizeof(uint32_t) * (size_t)slots));
-    ix.tag_slots = slots;
-    ix.tag_words = words;
-}
-
+// for a full-occupancy grid, allocated once at index load so that no search pays for it (at C5 a bitmap
+// workspace is 32 GB). Searches that need more (other LUT sizes, larger logs) still grow it. The lean kernel
+// keeps no visited table: with inline rows the bitmap waits for a search that needs it (another kernel, or
+// exact statistics).
 void reserve_search_scratch(DeviceIndex &ix)
 {
     int cus = 0;
@@ -1042,23 +1024,34 @@ void reserve_search_scratch(DeviceIndex &ix)
         return;
     const int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     const int slots = cus * per_cu;
-    if (ix.rows) { // the inline-row kernel's tagged words; the plain bitmap waits for a search that needs it
-        ensure_tagged(ix, slots);
-    } else {
+    if (!ix.rows) {
         ix.vis_words = std::max<int64_t>((ix.ntotal + 31) / 32, 1);
         ix.clear_cap = 16384;
         DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words, kBigVisited));
         DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)slots * (size_t)ix.vis_words));
         DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)slots * (size_t)ix.clear_cap));
         ix.n_slots = slots;
+        ix.device_bytes += (int64_t)sizeof(uint32_t) * slots * ix.vis_words + (int64_t)sizeof(int32_t) * slots * ix.clear_cap;
     }
     DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
+    DRM_HIP_CHECK(hipMemset(ix.counter, 0, 4 * sizeof(uint32_t)));
     const int cap = std::max(ix.log_cap_req, 128 + 64); // what the lean kernel asks for at ef = 128
     if (ix.log)
         DRM_HIP_CHECK(hipFree(ix.log));
     DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)slots * (size_t)cap));
     ix.log_cap = cap;
     ix.log_slots = slots;
+    ix.device_bytes += (int64_t)sizeof(uint64_t) * slots * cap;
+}
+
+void check_search_errors(const DeviceIndex &ix)
+{
+    if (!ix.counter)
+        return;
+    uint32_t c[4] = {0, 0, 0, 0};
+    DRM_HIP_CHECK(hipMemcpy(c, ix.counter, sizeof(c), hipMemcpyDeviceToHost));
+    if (c[3])
+        throw Error(DRM_ERR_INTERNAL, std::to_string(c[3]) + " queries exceeded the search's hop bound (ntotal hops)");
 }
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
@@ -1097,26 +1090,36 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix.device));
     int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
-    // (re)allocate per-slot workspace: the inline-row lean kernel uses the tagged words, the others the bitmap
+    // (re)allocate per-slot workspace: the lean kernel needs the bitmap only to count faiss's ndis
     const bool fast_path = ix.use_fast && !ix.try_sorted && hnsw_pq_fast_supported(ix, k, efc);
-    const bool tagged = fast_path && ix.rows != nullptr;
+    const bool need_bitmap = !fast_path || ix.exact_stats;
     const int64_t words = (ix.ntotal + 31) / 32;
-    if (tagged)
-        ensure_tagged(ix, std::max(slots, ix.tag_slots));
-    else if (slots > ix.n_slots || words != ix.vis_words) {
-        if (ix.visited)
+    if (need_bitmap && (slots > ix.n_slots || words != ix.vis_words)) {
+        if (ix.visited) {
             DRM_HIP_CHECK(hipFree(ix.visited));
-        if (ix.clear_list)
+            ix.device_bytes -= (int64_t)sizeof(uint32_t) * ix.n_slots * ix.vis_words;
+        }
+        if (ix.clear_list) {
             DRM_HIP_CHECK(hipFree(ix.clear_list));
+            ix.device_bytes -= (int64_t)sizeof(int32_t) * ix.n_slots * ix.clear_cap;
+        }
         ix.visited = nullptr;
         ix.clear_list = nullptr;
         const int alloc_slots = std::max(slots, (int)std::min<int64_t>((int64_t)cus * per_cu, 1 << 20));
         ix.vis_words = std::max<int64_t>(words, 1);
         ix.clear_cap = 16384;
+        size_t free_b = 0, total_b = 0;
+        DRM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        const size_t need_b = sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words +
+                              sizeof(int32_t) * (size_t)alloc_slots * (size_t)ix.clear_cap;
+        if (need_b > free_b)
+            throw Error(DRM_ERR_UNSUPPORTED, "the search's visited bitmaps need " + std::to_string(need_b >> 20) +
+                                                 " MiB of device memory, " + std::to_string(free_b >> 20) + " MiB free");
         DRM_HIP_CHECK(malloc_big((void **)&ix.visited, sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words, kBigVisited));
         DRM_HIP_CHECK(hipMemset(ix.visited, 0, sizeof(uint32_t) * (size_t)alloc_slots * (size_t)ix.vis_words));
         DRM_HIP_CHECK(hipMalloc(&ix.clear_list, sizeof(int32_t) * (size_t)alloc_slots * (size_t)ix.clear_cap));
         ix.n_slots = alloc_slots;
+        ix.device_bytes += (int64_t)(need_b);
     }
     if (!ix.counter)
         DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
@@ -1163,35 +1166,32 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     if (fast_path) {
         // the lean kernel (hnsw_pq_fast.hip); k == ef logs accepted pushes per slot
         const int cap = std::max(ix.log_cap_req, efc + 64); // one hop appends <= 64 after a compaction
-        const int need = std::max(tagged ? ix.tag_slots : ix.n_slots, slots);
+        const int need = std::max(ix.log_slots, slots);
         if (!ix.log || ix.log_cap != cap || ix.log_slots < need) {
-            if (ix.log)
+            if (ix.log) {
                 DRM_HIP_CHECK(hipFree(ix.log));
+                ix.device_bytes -= (int64_t)sizeof(uint64_t) * ix.log_slots * ix.log_cap;
+            }
             ix.log = nullptr;
             DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)need * (size_t)cap));
             ix.log_cap = cap;
             ix.log_slots = need;
-        }
-        if (tagged) {
-            a.visited = ix.vis_tag;
-            a.vis_words = ix.tag_words;
-            a.vis_gen = ix.vis_gen;
-            a.clear_list = nullptr;
-            a.clear_cap = 0;
+            ix.device_bytes += (int64_t)sizeof(uint64_t) * need * cap;
         }
         a.log = ix.log;
         a.log_cap = ix.log_cap;
         a.rows = ix.rows;
         a.row_words = ix.row_words;
         a.upper_codes = ix.upper_codes;
-        DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 3 * sizeof(uint32_t), stream));
-        launch_hnsw_pq_fast(a, slots, lds, ix.stamps != nullptr, stream);
+        a.exact_stats = ix.exact_stats;
+        DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 4 * sizeof(uint32_t), stream));
+        launch_hnsw_pq_fast(a, slots, ix.stamps != nullptr, stream);
         return;
     }
     // The sorted-array pass only pays off when distance ties are rare; stride-1 genome windows
     // share PQ codes so often that nearly every query falls back. Opt-in via DRM_SEARCH_SORTED=1.
     const bool sorted_path = ix.try_sorted && !ix.force_exact && vmode == 0 && R <= 2;
-    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 3 * sizeof(uint32_t), stream));
+    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 4 * sizeof(uint32_t), stream));
 #define DRM_LAUNCH_EXACT(RR, F8, VM)                                                                           \
     hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, F8>), dim3(slots), dim3(64), lds, stream, a)
 #define DRM_LAUNCH_EXACT_R(F8, VM)                                                                             \

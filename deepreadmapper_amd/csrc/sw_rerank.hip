@@ -363,8 +363,10 @@ constexpr int kNeedBitProfile = -4;
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
-#ifndef DRM_SW_ROWS2
-#define DRM_SW_ROWS2 1 // two DP rows in flight per pass (sw_row2_f16); 0: one row at a time (sw_row_f16)
+#ifndef DRM_SW_ROWS
+// DP rows in flight per pass over the columns, each one column behind the previous: 3 (sw_row3_i16), 2
+// (sw_row2_i16 / sw_row2_f16) or 1
+#define DRM_SW_ROWS 3
 #endif
 
 #ifndef DRM_SW_INT
@@ -471,6 +473,85 @@ __device__ __forceinline__ void sw_row2_i16(uint32_t (&H)[LQ], const uint32_t *p
         }
         best = imax3(best, ha, hb);
     }
+}
+
+// Three rows in flight (DRM_SW_ROWS 3): at step j rows a, b, c (candidate bytes i, i + 1, i + 2) compute columns j,
+// j - 1, j - 2, each from the value the row above has just written. Three independent left-to-right chains per wave
+// instead of two: the DP's issue rate is set by how many dependent max3 -> subtract chains a SIMD's waves hold
+// (one wave per SIMD ran at 46 % of two), and the 150-register row leaves room for two waves
+// only. Same ops per cell pair (the best takes one max3 per two cells); profile words of group g are refilled
+// once the last row (c) is past it.
+template <int LQ, int PF = 2>
+__device__ __forceinline__ void sw_row3_i16(uint32_t (&H)[LQ], const uint32_t *pa, const uint32_t *pb, const uint32_t *pc,
+                                            uint32_t &best)
+{
+    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
+    uint4 A[NS], B[NS], C[NS];
+#pragma unroll
+    for (int g = 0; g < NS; ++g)
+        if (g < NG) {
+            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
+            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
+            C[g] = *reinterpret_cast<const uint4 *>(pc + 4 * g);
+        }
+    auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
+    uint32_t tda = A[0].x, tdb = B[0].x, tdc = C[0].x; // column 0: zero-border diagonal
+    uint32_t lefta = 0u, leftb = 0u, leftc = 0u;
+    uint32_t hc_prev = 0u;
+#pragma clang loop unroll(full)
+    for (int j = 0; j <= LQ + 1; ++j) {
+        if ((j & 3) == 2 && j >= 6) { // group (j - 6) / 4 is done for all three rows: refill its slot
+            const int gd = (j - 6) >> 2, gn = gd + NS;
+            if (gn < NG) {
+                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
+                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
+                C[gd % NS] = *reinterpret_cast<const uint4 *>(pc + 4 * gn);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t ha = 0u, hb = 0u, hc = 0u;
+        if (j < LQ) {
+            const uint32_t up = H[j];
+            uint32_t tn = 0u;
+            if (j + 1 < LQ)
+                tn = up + word(A[((j + 1) >> 2) % NS], (j + 1) & 3);
+            const uint32_t h = idec(imax3(tda, up, lefta));
+            H[j] = h;
+            lefta = h;
+            tda = tn;
+            ha = h;
+        }
+        if (j >= 1 && j - 1 < LQ) {
+            const int c = j - 1;
+            const uint32_t up = H[c];
+            uint32_t tn = 0u;
+            if (c + 1 < LQ)
+                tn = up + word(B[((c + 1) >> 2) % NS], (c + 1) & 3);
+            const uint32_t h = idec(imax3(tdb, up, leftb));
+            H[c] = h;
+            leftb = h;
+            tdb = tn;
+            hb = h;
+        }
+        if (j >= 2) {
+            const int c = j - 2;
+            const uint32_t up = H[c];
+            uint32_t tn = 0u;
+            if (c + 1 < LQ)
+                tn = up + word(C[((c + 1) >> 2) % NS], (c + 1) & 3);
+            const uint32_t h = idec(imax3(tdc, up, leftc));
+            H[c] = h;
+            leftc = h;
+            tdc = tn;
+            hc = h;
+        }
+        best = imax3(best, ha, hb);
+        if (j & 1)
+            best = imax3(best, hc_prev, hc);
+        else
+            hc_prev = hc;
+    }
+    best = imax3(best, hc_prev, hc_prev); // LQ + 1 even: the last step's hc is still pending
 }
 
 __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
@@ -744,7 +825,15 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 return pprof + ka * GST + kb * PST;
             };
             int i = 0;
-#if DRM_SW_ROWS2
+#if DRM_SW_ROWS == 3 && DRM_SW_INT
+            for (; i + 2 < L; i += 3) {
+                const uint32_t *p0 = row(i);
+                const uint32_t *p1 = row(i + 1);
+                const uint32_t *p2 = row(i + 2);
+                sw_row3_i16<LQ>(H, p0, p1, p2, best);
+            }
+#endif
+#if DRM_SW_ROWS >= 2
             for (; i + 1 < L; i += 2) {
                 const uint32_t *p0 = row(i);
                 const uint32_t *p1 = row(i + 1);

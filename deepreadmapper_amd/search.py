@@ -52,6 +52,11 @@ class HnswPqIndex:
                                          d_nhops_upper.ptr if d_nhops_upper is not None else None,
                                          stream.handle if stream is not None else None))
 
+    def set_exact_stats(self, on=True):
+        """ndis as faiss counts it (links never visited before), from a visited bitmap kept for the count; off
+        (the default) the lean kernel reports the distances it computed. Results do not depend on it."""
+        check(lib().drm_index_set_exact_stats(self.handle, 1 if on else 0))
+
     def fallbacks(self):
         """Queries of the last search that met a distance tie and took the exact kernel (syncs)."""
         import ctypes as C

@@ -24,6 +24,7 @@ extern "C" {
 #define DRM_ERR_CANDS (-5)     /* "Not enough candidates (n < k)"  src/utils/reranker.cpp:26-29      */
 #define DRM_ERR_K (-6)         /* "Final k too large..."           src/utils/post_processor.cpp:486-489 */
 #define DRM_ERR_UNSUPPORTED (-7)
+#define DRM_ERR_INTERNAL (-8)  /* a kernel detected broken bookkeeping (e.g. a search past its hop bound)   */
 
 /* Threading: every handle (drm_index, drm_flat_index, drm_refs) owns mutable device scratch (visited
  * bitmaps, clear lists, queue counters, rerank workspace). A handle is single-stream: its calls must be
@@ -96,7 +97,10 @@ int drm_search(drm_index *index, const float *x, int64_t n, int32_t d, int32_t k
                drm_search_stats *stats);
 
 /* Same search on device-resident buffers, enqueued on `stream` (a hipStream_t, NULL = default).
- * ndis / nhops ([n] int32, may be NULL) receive the per-query HNSWStats the kernel measured. */
+ * ndis / nhops ([n] int32, may be NULL) receive the per-query HNSWStats the kernel measured: nhops always as
+ * faiss counts it; ndis as faiss counts it (links never seen before) with drm_index_set_exact_stats on, else, on
+ * the PQ 8x8 lean kernel, the distances the kernel computed. A query that exceeded its hop bound (broken
+ * bookkeeping, never expected) reports nhops = ndis = -1; drm_search turns that into DRM_ERR_INTERNAL. */
 int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                       int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, void *stream);
 /* As drm_search_device, plus d_nhops_upper[n] (may be NULL): the greedy hops on levels >= 1
@@ -108,6 +112,11 @@ int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t 
  * for a rerank kernel running beside the search on another stream (drm_refs_set_sw_waves). Results do
  * not depend on it. */
 int drm_index_set_search_waves(drm_index *index, int32_t waves_per_cu);
+/* Statistics (no reference counterpart): on (1), ndis counts faiss's HNSWStats.ndis exactly -- the links each
+ * hop finds not yet visited -- with a per-slot visited bitmap kept beside the search (the lean kernel needs none
+ * for its results). Off (0, the default; DRM_SEARCH_EXACT_STATS=1 at load sets it) the lean
+ * kernel reports the distances it computed. Results (D, I, nhops) do not depend on it. */
+int drm_index_set_exact_stats(drm_index *index, int32_t on);
 /* Diagnostic (no reference counterpart): how many queries of the last search on this index met an
  * exact distance tie and were re-run by the exact (faiss heap-layout) kernel. Synchronizes the device. */
 int drm_search_fallbacks(drm_index *index, int64_t *count);

@@ -64,3 +64,35 @@ def test_two_rank_gather_equals_single_process(c1, tmp_path):
     rc, sc, ids, cnt = O.post_process_sw_static(I, c1["refs"], 150, qbuf, ql, 1, 32, 32, nthreads=1)
     assert np.array_equal(g["I"], I) and np.array_equal(g["D"].view(np.uint32), D.view(np.uint32))
     assert np.array_equal(g["S"], sc)
+
+
+def _verdict_worker(rank, world, port, mode, out_path):
+    """One rank of a gloo job calling bench.gather_verdict with a gather result forced per `mode`."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    D = bench.Dist()
+    good = {"backend": "RCCL", "ms": 1.0, "rows": 10}
+    if rank == 0:
+        good["rank0_shard_matches"] = mode != "mismatch"
+    gather = {"error": "RuntimeError: forced"} if (mode == "error" and rank == 1) else (
+        {"skipped": "2 ranks share 1 device(s)"} if mode == "skipped" else good)
+    v = bench.gather_verdict(D, gather)
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(v, f)
+    D.close()
+
+
+@pytest.mark.parametrize("mode,expect", [("ok", True), ("error", False), ("mismatch", False), ("skipped", None)])
+def test_bench_gather_verdict_two_ranks(tmp_path, mode, expect):
+    """bench.py at N > 1: a gather error on any rank (here rank 1 only) or a rank-0 shard mismatch fails the job on
+    every rank (gather_ok false, non-zero exit); a gather skipped because ranks share a device is not checked."""
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "v")
+    mp.spawn(_verdict_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
+    for r in range(2):
+        assert json.load(open(f"{out}.{r}")) == expect

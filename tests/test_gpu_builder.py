@@ -69,6 +69,7 @@ def test_gpu_build_c1_layout_and_search_parity(tmp_path, c1):
             assert (seg[:len(v)] >= 0).all() and i not in v and len(set(v.tolist())) == len(v)
             assert (fg.levels[v] > l).all()
     ix = read_index(gpu)
+    ix.set_exact_stats(True)  # ndis as faiss counts it
     D, I, st = ix.search(c1["q"], 128, 128)
     ix.free()
     Do, Io, nd, nh = O.hnswpq_search(fg, c1["q"], 128, 128)

@@ -33,6 +33,7 @@ def test_c5_search_and_rerank_vs_oracle(c5):
     from oracle import faiss_file, oracle as O
     K = EF = 128
     ix = read_index(c5["index"])
+    ix.set_exact_stats(True)  # ndis as faiss counts it (the full-slice test runs the default mode)
     D, I, st = ix.search(c5["x"], K, EF)
     fx = faiss_file.read(c5["index"])
     Do, Io, nd, nh = O.hnswpq_search(fx, c5["x"], K, EF)

@@ -151,13 +151,19 @@ def test_sw_reranker_api():
 
 # ------------------------------------------------------------------------------------------ search
 def _search_both(index_path, fx, q, k, ef):
+    """The default search (ids, 0-ulp distances, nhops) and the exact-statistics search (the same, plus faiss's
+    ndis) against the oracle."""
     from deepreadmapper_amd import read_index
     ix = read_index(index_path)
     D, I, st = ix.search(q, k, ef)
     Do, Io, nd, nh = O.hnswpq_search(fx, q, k, ef)
     assert np.array_equal(I, Io)
     assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))  # 0-ulp fp32
-    assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+    assert st.nhops == int(nh.sum())
+    ix.set_exact_stats(True)
+    D2, I2, st2 = ix.search(q, k, ef)
+    assert np.array_equal(I2, Io) and np.array_equal(D2.view(np.uint32), Do.view(np.uint32))
+    assert st2.ndis == int(nd.sum()) and st2.nhops == int(nh.sum())
     ix.free()
     return D, I
 
@@ -179,38 +185,83 @@ def test_search_syn20k_bitexact(syn20k):
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
 
 
-def test_search_visited_generation_wrap(syn20k):
-    """The inline-row lean kernel tags each visited word with the query's 16-bit generation instead of clearing
-    its bits after every query. Generations set just below the wrap, and a small grid (256 slots, ~8 queries
-    each), make every slot restart its words mid-batch: results stay bit-identical to the oracle, across
-    repeated launches on one handle and across K = 128 / K = 5 (both variants share the generations). The hook
-    restarts the words at the generation it sets (generations only ever increase between wraps)."""
-    import ctypes as C
+def test_search_heap_visited_repeated_launches(syn20k):
+    """The lean kernel keeps no visited table (its heap is the visited set): nothing carries over between queries
+    or launches. A small grid (1 wave per CU, ~80 queries per slot), repeated launches on one handle, K = 128 / K = 5
+    interleaved and the exact-statistics mode switched on and off between them all give the oracle's results."""
     from deepreadmapper_amd import read_index
     from deepreadmapper_amd._native import check, lib
     w, fx = syn20k["w"], syn20k["fx"]
     q = w.q_emb
-    L = lib()
-    L.drm_debug_search_generation.argtypes = [C.c_void_p, C.c_uint32]
     ix = read_index(syn20k["index"])
-    check(L.drm_index_set_search_waves(ix.handle, 1))
+    check(lib().drm_index_set_search_waves(ix.handle, 1))
     Do, Io, nd, nh = O.hnswpq_search(fx, q, 128, 128)
     D5o, I5o, nd5, nh5 = O.hnswpq_search(fx, q, 5, 128)
-    for gen in (0xFFFD, 0xFFFF, 7):
-        check(L.drm_debug_search_generation(ix.handle, gen))
+    for stats in (False, True, False):
+        ix.set_exact_stats(stats)
         for _ in range(2):
             D, I, st = ix.search(q, 128, 128)
             bad = np.flatnonzero((I != Io).any(axis=1))
-            assert bad.size == 0, f"generation {gen:#x}: {bad.size} rows differ, first {bad[:8]}"
+            assert bad.size == 0, f"stats={stats}: {bad.size} rows differ, first {bad[:8]}"
             assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))
-            assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
+            assert st.nhops == int(nh.sum()) and (not stats or st.ndis == int(nd.sum()))
             D5, I5, st5 = ix.search(q, 5, 128)
-            assert np.array_equal(I5, I5o) and np.array_equal(D5.view(np.uint32), D5o.view(np.uint32)), f"{gen:#x}"
-            assert st5.ndis == int(nd5.sum()) and st5.nhops == int(nh5.sum())
-    check(L.drm_index_set_search_waves(ix.handle, 0))
+            assert np.array_equal(I5, I5o) and np.array_equal(D5.view(np.uint32), D5o.view(np.uint32))
+            assert st5.nhops == int(nh5.sum()) and (not stats or st5.ndis == int(nd5.sum()))
+    check(lib().drm_index_set_search_waves(ix.handle, 0))
     D, I, st = ix.search(q, 128, 128)
-    assert np.array_equal(I, Io) and st.ndis == int(nd.sum())
+    assert np.array_equal(I, Io) and st.nhops == int(nh.sum())
     ix.free()
+
+
+@pytest.mark.parametrize("fast", ["1", "0"])
+def test_search_tie_fixtures(tmp_path, fast, monkeypatch):
+    """The hand-derived traversal fixtures (tests/golden/hnsw_tie_cases.json: pop_min among equal minima, the
+    v >= dis[0] rejection at equality, result insertion order among equal distances, a duplicate link, upper-level
+    ties) through the lean kernel (default and exact statistics) and the general kernel (DRM_SEARCH_FAST=0); then 40
+    random tie-heavy graphs against the C oracle."""
+    import tie_graphs as TG
+    from deepreadmapper_amd import read_index
+    from oracle import faiss_file
+    monkeypatch.setenv("DRM_SEARCH_FAST", fast)
+    q = np.zeros((1, TG.D), dtype=np.float32)
+    for case in TG.load_cases():
+        ix = read_index(TG.write_case(case, str(tmp_path)))
+        e = case["expected"]
+        for stats in (False, True):
+            ix.set_exact_stats(stats)
+            D, I, st = ix.search(q, case["k"], case["ef"])
+            assert I[0].tolist() == e["I"] and D[0].tolist() == e["D"], (case["name"], stats)
+            assert st.nhops == e["nhops"], case["name"]
+            if stats or fast == "0":
+                assert st.ndis == e["ndis"], case["name"]
+        ix.free()
+    rng = np.random.default_rng(77)
+    for g in range(40):
+        rows, codes, entry, max_level = TG.random_tie_graph(rng, int(rng.integers(6, 41)))
+        path = TG.write_ihnp(str(tmp_path / f"r{g}.index"), rows, codes, entry, max_level)
+        fx = faiss_file.read(path)
+        qq = np.zeros((3, TG.D), dtype=np.float32)
+        qq[1, 0] = float(rng.integers(1, 12))
+        qq[2] = rng.standard_normal(TG.D).astype(np.float32)
+        ix = read_index(path)
+        ix.set_exact_stats(True)
+        for k, ef in ((1, 1), (2, 3), (3, 3), (4, 2), (5, 8), (8, 8)):
+            D, I, st = ix.search(qq, k, ef)
+            Do, Io, nd, nh = O.hnswpq_search(fx, qq, k, ef)
+            assert np.array_equal(I, Io) and np.array_equal(D.view(np.uint32), Do.view(np.uint32)), (g, k, ef)
+            assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum()), (g, k, ef)
+        ix.free()
+
+
+def test_search_committed_c1_fixture():
+    """The committed C1 IHNp file and queries (tests/golden/make_c1_index.py) give the committed expected rows."""
+    from deepreadmapper_amd import read_index
+    exp = np.load(os.path.join(GOLDEN, "c1_expected_k128_ef128.npz"))
+    ix = read_index(os.path.join(GOLDEN, "c1_hnswpq.index"))
+    D, I, st = ix.search(np.load(os.path.join(GOLDEN, "c1_queries.npy")), 128, 128)
+    ix.free()
+    assert np.array_equal(I, exp["I"]) and np.array_equal(D.view(np.uint32), exp["D"].view(np.uint32))
 
 
 def test_search_syn20k_sorted_pass(syn20k, monkeypatch):

@@ -80,13 +80,18 @@ def _check_search(index_path, fx, q, k, ef, ntotal):
     Do, Io, ndo, nho = O.hnswpq_search(fx, q[s], k, ef, nthreads=_threads())
     assert np.array_equal(I[s], Io)
     assert np.array_equal(D[s].view(np.uint32), Do.view(np.uint32))  # 0 ulp
-    assert np.array_equal(nd[s], ndo) and np.array_equal(nh[s], nho)
-    # the same queries searched alone give the same rows as inside the full batch
+    assert np.array_equal(nh[s], nho)
+    # the same queries searched alone give the same rows as inside the full batch, and with exact statistics
+    # the same rows plus faiss's ndis
     from deepreadmapper_amd import read_index
     ix = read_index(index_path)
     D2, I2, _ = ix.search(q[s[:256]], k, ef)
+    ix.set_exact_stats(True)
+    D3, I3, st3 = ix.search(q[s[:256]], k, ef)
     ix.free()
     assert np.array_equal(I2, I[s[:256]]) and np.array_equal(D2.view(np.uint32), D[s[:256]].view(np.uint32))
+    assert np.array_equal(I3, I2) and np.array_equal(D3.view(np.uint32), D2.view(np.uint32))
+    assert st3.ndis == int(ndo[:256].sum()) and st3.nhops == int(nho[:256].sum())
     return D, I
 
 
