@@ -136,20 +136,12 @@ struct ExecCache {
     {
         device = dev;
         HC(hipSetDevice(dev));
-        // HIP deals its streams round-robin over GPU_MAX_HW_QUEUES hardware queues (4 on the box), and two
-        // streams on one queue run in submission order: measured, the 5th stream of a process serialises with
-        // the 1st (tools/microbench/concurrency.hip). A stream with a CU mask gets a hardware queue of its own;
-        // with every CU in the mask it is an ordinary stream that never shares its queue.
-        int cus = 0;
-        HC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        std::vector<uint32_t> mask((size_t)std::max(1, (cus + 31) / 32), 0u);
-        for (int c = 0; c < cus; ++c)
-            mask[(size_t)c / 32] |= 1u << (c % 32);
+        // two non-blocking streams (no implicit synchronisation with the legacy null stream). HIP deals its
+        // streams round-robin over GPU_MAX_HW_QUEUES hardware queues (4 on the box) and two streams on one queue
+        // run in submission order (tools/microbench/concurrency.hip); the executor's own two streams are created
+        // together, so they land on different queues.
         for (hipStream_t *s : {&s_search, &s_sw})
-            if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-                (void)hipGetLastError();
-                HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-            }
+            HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         HC(hipEventCreate(&e0));
         HC(hipEventCreate(&e1));
         for (auto &b : sets)
@@ -466,9 +458,12 @@ void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, in
     auto *pp = genome_mode ? drm_post_process_sw_dynamic_device : drm_post_process_sw_static_device;
     const size_t kc = (size_t)k_clusters, kr = (size_t)k;
     auto lo_of = [&](int b) { return n * b / P; };
+    const bool overlap = P > 1 && co.search_waves > 0 && co.sw_waves > 0;
+    // the grid caps are touched only when batches overlap (a caller's own setting is left alone otherwise)
     auto search = [&](int b, int waves) {
         const int64_t lo = lo_of(b), m = lo_of(b + 1) - lo;
-        abi_check(drm_index_set_search_waves(index, waves));
+        if (overlap)
+            abi_check(drm_index_set_search_waves(index, waves));
         HC(hipEventRecord(ex.ev_ss[(size_t)b], ex.s_search));
         abi_check(drm_search_device_ex(index, d_x + (size_t)lo * info.d, m, k_clusters, ef, d_D + (size_t)lo * kc,
                                        d_I + (size_t)lo * kc, d_ndis ? d_ndis + lo : nullptr,
@@ -478,7 +473,8 @@ void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, in
     };
     auto rerank = [&](int b, int waves) {
         const int64_t lo = lo_of(b), m = lo_of(b + 1) - lo;
-        abi_check(drm_refs_set_sw_waves(refs, waves));
+        if (overlap)
+            abi_check(drm_refs_set_sw_waves(refs, waves));
         HC(hipStreamWaitEvent(ex.s_sw, ex.ev_se[(size_t)b], 0));
         HC(hipEventRecord(ex.ev_ws[(size_t)b], ex.s_sw));
         abi_check(pp(refs, d_I + (size_t)lo * kc, m, k_clusters, d_queries + (size_t)lo * q_stride, d_q_len + lo,
@@ -490,7 +486,6 @@ void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, in
         HC(hipEventRecord(ex.join, stream)); // both streams start behind the caller's earlier work
         HC(hipStreamWaitEvent(ex.s_search, ex.join, 0));
         HC(hipStreamWaitEvent(ex.s_sw, ex.join, 0));
-        const bool overlap = P > 1 && co.search_waves > 0 && co.sw_waves > 0;
         for (int b = 0; b < P; ++b) {
             if (b >= 2) // phase lock: search(b) starts beside rerank(b-1), after rerank(b-2)
                 HC(hipStreamWaitEvent(ex.s_search, ex.ev_we[(size_t)b - 2], 0));
@@ -499,13 +494,17 @@ void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, in
                 rerank(b - 1, overlap ? co.sw_waves : 0);
         }
         rerank(P - 1, 0); // alone: the full grid
-        abi_check(drm_index_set_search_waves(index, 0));
-        abi_check(drm_refs_set_sw_waves(refs, 0));
+        if (overlap) {
+            abi_check(drm_index_set_search_waves(index, 0));
+            abi_check(drm_refs_set_sw_waves(refs, 0));
+        }
         HC(hipStreamWaitEvent(stream, ex.ev_se[(size_t)P - 1], 0));
         HC(hipStreamWaitEvent(stream, ex.ev_we[(size_t)P - 1], 0));
     } catch (...) {
-        (void)drm_index_set_search_waves(index, 0);
-        (void)drm_refs_set_sw_waves(refs, 0);
+        if (overlap) {
+            (void)drm_index_set_search_waves(index, 0);
+            (void)drm_refs_set_sw_waves(refs, 0);
+        }
         ex.drain();
         throw;
     }

@@ -364,24 +364,18 @@ constexpr int kNeedBitProfile = -4;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 #ifndef DRM_SW_ROWS
-// DP rows in flight per pass over the columns, each one column behind the previous: 3 (sw_row3_i16), 2
-// (sw_row2_i16 / sw_row2_f16) or 1
-#define DRM_SW_ROWS 3
+#define DRM_SW_ROWS 3 // DP rows in flight per pass over the columns (sw_rows_i16)
+#endif
+#ifndef DRM_SW_PF
+#define DRM_SW_PF 2 // profile groups (4 columns each) read ahead of the one in use, per row
 #endif
 
-#ifndef DRM_SW_INT
-// 1: scores as 16-bit integers (two per register), the diagonal add as one 32-bit add over both halves, the
-// three-way max as v_pk_maximum3_f16 on the integer bit patterns, the -1 floored at 0 as a saturating packed
-// subtract (sw_row_i16 / sw_row2_i16); 0: fp16 multiples of 2^-10 (sw_row_f16 / sw_row2_f16)
-#define DRM_SW_INT 1
-#endif
-
-// ---- integer cells (DRM_SW_INT). A score s (0 <= s <= 1023) is the 16-bit pattern s, i.e. the fp16 subnormal
-// s * 2^-24: fp16 ordering of non-negative patterns below 0x7C00 is the integer ordering (subnormals included:
-// fp16 denormals are kept, the default FP mode), so v_pk_maximum3_f16 is an exact integer max3. The diagonal
-// term (+2 on a match) is added by v_add_u32 across both halves: the low half stays below 2^16 (s <= 1023 + 2),
-// so no carry crosses. One cell pair costs a 32-bit add (2 cycles per wave64 instruction on gfx950) instead of a
-// packed add (4 cycles), profiles/r02/valu_rate_probe.txt: 12 instead of 14 issue cycles per cell pair.
+// ---- integer cells. A score s (0 <= s <= 1023) is the 16-bit pattern s, i.e. the fp16 subnormal s * 2^-24: fp16
+// ordering of non-negative patterns below 0x7C00 is the integer ordering (subnormals included: fp16 denormals are
+// kept, the default FP mode), so v_pk_maximum3_f16 is an exact integer max3. The diagonal term (+2 on a match) is
+// added by v_add_u32 across both halves: the low half stays below 2^16 (s <= 1023 + 2), so no carry crosses. One
+// cell pair costs a 32-bit add (2 cycles per wave64 instruction on gfx950), a packed max3 and a packed saturating
+// subtract (4 each), and half a packed max3 for the best: 12 issue cycles (profiles/r02/valu_rate_probe.txt).
 __device__ __forceinline__ uint32_t imax3(uint32_t a, uint32_t b, uint32_t c)
 {
     const h2 r = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b)),
@@ -394,164 +388,75 @@ __device__ __forceinline__ uint32_t idec(uint32_t a) // max(0, s - 1) in both ha
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a), (u16x2){1, 1}));
 }
 
-template <int LQ>
-__device__ __forceinline__ void sw_row_i16(uint32_t (&H)[LQ], const uint32_t *pp, uint32_t &best)
+// R DP rows in one pass over the LQ columns (rows = consecutive candidate bytes i .. i + R - 1): at step j row r
+// computes column j - r, from the value the row above it wrote there one step earlier, so one wave issues from R
+// independent left-to-right chains (max3 -> subtract -> the next column's max3) instead of one. The DP row lives
+// in H (one register per column, two candidates per register) and is updated in place: a cell's next-column
+// diagonal term is formed from H[c] before the cell overwrites it. The issue rate of this DP is set by the number
+// of such chains a SIMD holds (one wave per SIMD ran at 46 % of two; the 150-register row
+// leaves room for two waves only), so R is the lever. Per row, the profile words of PF groups of 4 columns are
+// read ahead of the one in use (one ds_read_b128 each), and a group's slot is refilled once the last row is past
+// it. The best takes one max3 per two cells. pp[r]: the pair-profile row of DP row i + r (match terms of the two
+// candidates' bytes against every query column).
+template <int LQ, int R, int PF>
+__device__ __forceinline__ void sw_rows_i16(uint32_t (&H)[LQ], const uint32_t *const (&pp)[R], uint32_t &best)
 {
-    uint4 P = *reinterpret_cast<const uint4 *>(pp);
-    uint32_t td = P.x; // column 0: the diagonal is the zero border
-    uint32_t left = 0u;
-#pragma unroll
-    for (int j = 0; j < LQ; ++j) {
-        const uint32_t up = H[j];
-        uint32_t tn = 0u;
-        if (j + 1 < LQ) {
-            const int n = j + 1;
-            if ((n & 3) == 0)
-                P = *reinterpret_cast<const uint4 *>(pp + n);
-            tn = up + ((n & 3) == 0 ? P.x : (n & 3) == 1 ? P.y : (n & 3) == 2 ? P.z : P.w);
-        }
-        const uint32_t h = idec(imax3(td, up, left));
-        H[j] = h;
-        left = h;
-        best = imax3(best, h, h);
-        td = tn;
-    }
-}
-
-// sw_row2_f16's two-rows-in-flight schedule on integer cells
-template <int LQ, int PF = 2>
-__device__ __forceinline__ void sw_row2_i16(uint32_t (&H)[LQ], const uint32_t *pa, const uint32_t *pb, uint32_t &best)
-{
-    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
-    uint4 A[NS], B[NS];
+    constexpr int NG = (LQ + 3) / 4, NS = PF + 1, LAG = R - 2;
+    uint4 P[R][NS];
 #pragma unroll
     for (int g = 0; g < NS; ++g)
-        if (g < NG) {
-            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
-            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
-        }
-    auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
-    uint32_t tda = A[0].x, tdb = B[0].x; // column 0: zero-border diagonal
-    uint32_t lefta = 0u, leftb = 0u;
-#pragma clang loop unroll(full)
-    for (int j = 0; j <= LQ; ++j) {
-        if ((j & 3) == 0 && j >= 4) {
-            const int gd = (j >> 2) - 1, gn = gd + NS;
-            if (gn < NG) {
-                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
-                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        uint32_t ha = 0u, hb = 0u;
-        if (j < LQ) {
-            const uint32_t up = H[j];
-            uint32_t tn = 0u;
-            if (j + 1 < LQ) {
-                const int n = j + 1;
-                tn = up + word(A[(n >> 2) % NS], n & 3);
-            }
-            const uint32_t h = idec(imax3(tda, up, lefta));
-            H[j] = h;
-            lefta = h;
-            tda = tn;
-            ha = h;
-        }
-        if (j >= 1) {
-            const int c = j - 1;
-            const uint32_t up = H[c];
-            uint32_t tn = 0u;
-            if (c + 1 < LQ) {
-                const int n = c + 1;
-                tn = up + word(B[(n >> 2) % NS], n & 3);
-            }
-            const uint32_t h = idec(imax3(tdb, up, leftb));
-            H[c] = h;
-            leftb = h;
-            tdb = tn;
-            hb = h;
-        }
-        best = imax3(best, ha, hb);
-    }
-}
-
-// Three rows in flight (DRM_SW_ROWS 3): at step j rows a, b, c (candidate bytes i, i + 1, i + 2) compute columns j,
-// j - 1, j - 2, each from the value the row above has just written. Three independent left-to-right chains per wave
-// instead of two: the DP's issue rate is set by how many dependent max3 -> subtract chains a SIMD's waves hold
-// (one wave per SIMD ran at 46 % of two), and the 150-register row leaves room for two waves
-// only. Same ops per cell pair (the best takes one max3 per two cells); profile words of group g are refilled
-// once the last row (c) is past it.
-template <int LQ, int PF = 2>
-__device__ __forceinline__ void sw_row3_i16(uint32_t (&H)[LQ], const uint32_t *pa, const uint32_t *pb, const uint32_t *pc,
-                                            uint32_t &best)
-{
-    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
-    uint4 A[NS], B[NS], C[NS];
 #pragma unroll
-    for (int g = 0; g < NS; ++g)
-        if (g < NG) {
-            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
-            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
-            C[g] = *reinterpret_cast<const uint4 *>(pc + 4 * g);
-        }
+        for (int r = 0; r < R; ++r)
+            if (g < NG)
+                P[r][g] = *reinterpret_cast<const uint4 *>(pp[r] + 4 * g);
     auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
-    uint32_t tda = A[0].x, tdb = B[0].x, tdc = C[0].x; // column 0: zero-border diagonal
-    uint32_t lefta = 0u, leftb = 0u, leftc = 0u;
-    uint32_t hc_prev = 0u;
-#pragma clang loop unroll(full)
-    for (int j = 0; j <= LQ + 1; ++j) {
-        if ((j & 3) == 2 && j >= 6) { // group (j - 6) / 4 is done for all three rows: refill its slot
-            const int gd = (j - 6) >> 2, gn = gd + NS;
-            if (gn < NG) {
-                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
-                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
-                C[gd % NS] = *reinterpret_cast<const uint4 *>(pc + 4 * gn);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        uint32_t ha = 0u, hb = 0u, hc = 0u;
-        if (j < LQ) {
-            const uint32_t up = H[j];
-            uint32_t tn = 0u;
-            if (j + 1 < LQ)
-                tn = up + word(A[((j + 1) >> 2) % NS], (j + 1) & 3);
-            const uint32_t h = idec(imax3(tda, up, lefta));
-            H[j] = h;
-            lefta = h;
-            tda = tn;
-            ha = h;
-        }
-        if (j >= 1 && j - 1 < LQ) {
-            const int c = j - 1;
-            const uint32_t up = H[c];
-            uint32_t tn = 0u;
-            if (c + 1 < LQ)
-                tn = up + word(B[((c + 1) >> 2) % NS], (c + 1) & 3);
-            const uint32_t h = idec(imax3(tdb, up, leftb));
-            H[c] = h;
-            leftb = h;
-            tdb = tn;
-            hb = h;
-        }
-        if (j >= 2) {
-            const int c = j - 2;
-            const uint32_t up = H[c];
-            uint32_t tn = 0u;
-            if (c + 1 < LQ)
-                tn = up + word(C[((c + 1) >> 2) % NS], (c + 1) & 3);
-            const uint32_t h = idec(imax3(tdc, up, leftc));
-            H[c] = h;
-            leftc = h;
-            tdc = tn;
-            hc = h;
-        }
-        best = imax3(best, ha, hb);
-        if (j & 1)
-            best = imax3(best, hc_prev, hc);
-        else
-            hc_prev = hc;
+    uint32_t td[R], left[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        td[r] = P[r][0].x; // column 0: the diagonal is the zero border
+        left[r] = 0u;
     }
-    best = imax3(best, hc_prev, hc_prev); // LQ + 1 even: the last step's hc is still pending
+    uint32_t pend = 0u; // R odd: the last row's value of an even step, paired with the next step's
+#pragma clang loop unroll(full)
+    for (int j = 0; j < LQ + R - 1; ++j) {
+        if (j - LAG >= 4 && ((j - LAG) & 3) == 0) { // group gd is done for every row: refill its slot
+            const int gd = ((j - LAG) >> 2) - 1, gn = gd + NS;
+            if (gn < NG) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    P[r][gd % NS] = *reinterpret_cast<const uint4 *>(pp[r] + 4 * gn);
+            }
+            __builtin_amdgcn_sched_barrier(0); // keep the reads here, ahead of the columns that consume them
+        }
+        uint32_t h[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int c = j - r;
+            h[r] = 0u;
+            if (c >= 0 && c < LQ) {
+                const uint32_t up = H[c];
+                uint32_t tn = 0u;
+                if (c + 1 < LQ)
+                    tn = up + word(P[r][((c + 1) >> 2) % NS], (c + 1) & 3);
+                const uint32_t v = idec(imax3(td[r], up, left[r]));
+                H[c] = v;
+                left[r] = v;
+                td[r] = tn;
+                h[r] = v;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r + 1 < R; r += 2)
+            best = imax3(best, h[r], h[r + 1]);
+        if (R & 1) {
+            if (j & 1)
+                best = imax3(best, pend, h[R - 1]);
+            else
+                pend = h[R - 1];
+        }
+    }
+    if (R & 1)
+        best = imax3(best, pend, pend);
 }
 
 __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything else -> -1
@@ -560,105 +465,6 @@ __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything els
     return (((0x47544341u >> (8 * k)) & 0xFFu) == (uint32_t)c) ? k : -1;
 }
 __device__ __forceinline__ int acgt_byte(int k) { return k < 4 ? (int)((0x47544341u >> (8 * k)) & 0xFFu) : -1; }
-
-template <int LQ>
-__device__ __forceinline__ void sw_row_f16(h2 (&H)[LQ], const uint32_t *pp, h2 &best)
-{
-    const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
-    const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
-    uint4 P = *reinterpret_cast<const uint4 *>(pp);
-    h2 td = __builtin_bit_cast(h2, P.x); // column 0: the diagonal is the zero border
-    h2 left = kZero;
-#pragma unroll
-    for (int j = 0; j < LQ; ++j) {
-        const h2 up = H[j];
-        // the next column's diag + term is formed from old H[j] before H[j] is overwritten, so H
-        // stays in place across rows (no register rotation)
-        h2 tn = kZero;
-        if (j + 1 < LQ) {
-            const int n = j + 1;
-            if ((n & 3) == 0)
-                P = *reinterpret_cast<const uint4 *>(pp + n);
-            const uint32_t w = (n & 3) == 0 ? P.x : (n & 3) == 1 ? P.y : (n & 3) == 2 ? P.z : P.w;
-            tn = up + __builtin_bit_cast(h2, w);
-        }
-        h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(td, up), left);
-        h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
-        H[j] = h;
-        left = h;
-        best = __builtin_elementwise_maximum(best, h);
-        td = tn;
-    }
-}
-
-// Two DP rows at once, the second one column behind the first: at step j row a (candidate byte i) computes
-// column j and row b (byte i + 1) column j - 1, from the value row a has just written there. The two rows'
-// left-to-right dependency chains (max3 -> clamp -> next max3) are independent, so one wave issues from two
-// chains instead of one -- the op count per cell pair is unchanged (3.5), but a single wave per SIMD no
-// longer stalls on every cell's dependency: the rerank can then run one wave per SIMD
-// beside the search kernel.
-template <int LQ, int PF = 2>
-__device__ __forceinline__ void sw_row2_f16(h2 (&H)[LQ], const uint32_t *pa, const uint32_t *pb, h2 &best)
-{
-    const h2 kMinusDelta = {(_Float16)-0.0009765625f, (_Float16)-0.0009765625f}; // -2^-10
-    const h2 kZero = {(_Float16)0.0f, (_Float16)0.0f}, kOne = {(_Float16)1.0f, (_Float16)1.0f};
-    // the profile words of both rows, 4 columns (one ds_read_b128) per group, PF groups in flight ahead of the
-    // one being consumed: a group's slot is refilled once both rows are past it. At one wave per SIMD nothing
-    // else hides the LDS latency, so the reads are issued ~8 columns (112 VALU) before their use.
-    constexpr int NG = (LQ + 3) / 4, NS = PF + 1;
-    uint4 A[NS], B[NS];
-#pragma unroll
-    for (int g = 0; g < NS; ++g)
-        if (g < NG) {
-            A[g] = *reinterpret_cast<const uint4 *>(pa + 4 * g);
-            B[g] = *reinterpret_cast<const uint4 *>(pb + 4 * g);
-        }
-    auto word = [](const uint4 &v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
-    h2 tda = __builtin_bit_cast(h2, A[0].x), tdb = __builtin_bit_cast(h2, B[0].x); // column 0: zero-border diagonal
-    h2 lefta = kZero, leftb = kZero;
-#pragma clang loop unroll(full)
-    for (int j = 0; j <= LQ; ++j) {
-        if ((j & 3) == 0 && j >= 4) { // group j/4 - 1 is done for both rows: refill its slot
-            const int gd = (j >> 2) - 1, gn = gd + NS;
-            if (gn < NG) {
-                A[gd % NS] = *reinterpret_cast<const uint4 *>(pa + 4 * gn);
-                B[gd % NS] = *reinterpret_cast<const uint4 *>(pb + 4 * gn);
-            }
-            __builtin_amdgcn_sched_barrier(0); // keep the reads here, ahead of the columns that consume them
-        }
-        h2 ha = kZero, hb = kZero;
-        if (j < LQ) { // row a, column j: up = the previous row's H[j]
-            const h2 up = H[j];
-            h2 tn = kZero;
-            if (j + 1 < LQ) {
-                const int n = j + 1;
-                tn = up + __builtin_bit_cast(h2, word(A[(n >> 2) % NS], n & 3));
-            }
-            h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tda, up), lefta);
-            h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
-            H[j] = h;
-            lefta = h;
-            tda = tn;
-            ha = h;
-        }
-        if (j >= 1) { // row b, column c = j - 1: up = row a's value, written at the previous step
-            const int c = j - 1;
-            const h2 up = H[c];
-            h2 tn = kZero;
-            if (c + 1 < LQ) {
-                const int n = c + 1;
-                tn = up + __builtin_bit_cast(h2, word(B[(n >> 2) % NS], n & 3));
-            }
-            h2 h = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tdb, up), leftb);
-            h = __builtin_elementwise_min(__builtin_elementwise_max(h + kMinusDelta, kZero), kOne);
-            H[c] = h;
-            leftb = h;
-            tdb = tn;
-            hb = h;
-        }
-        best = __builtin_elementwise_maximum(__builtin_elementwise_maximum(best, ha), hb);
-    }
-}
 
 // Kernel 1 (fast path) of the rerank: candidate lists (find_sequences static) + one SW score per
 // candidate; same contract as sw_score_kernel. One 64-lane workgroup per query (grid-stride).
@@ -740,8 +546,8 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             uint32_t word = 0;
             if (kb < 5 && j < qe && j < LQ) {
                 const int c = qbuf[lead + j];
-                // the diagonal term: +2 on a match (the -1 every cell takes makes it +1), 2^-9 in the fp16 form
-                const uint32_t t = DRM_SW_INT ? 0x0002u : 0x1800u;
+                // the diagonal term: +2 on a match (the -1 every cell takes makes it +1)
+                const uint32_t t = 0x0002u;
                 word = (c == acgt_byte(ka) ? t : 0u) | (c == acgt_byte(kb) ? t << 16 : 0u);
             }
             pprof[e] = word;
@@ -755,19 +561,11 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         for (int c0 = tid; c0 < (qe > LQ ? 0 : ncand); c0 += 128) {
             const int c1 = c0 + 64;
             const bool has_b = c1 < ncand;
-#if DRM_SW_INT
             uint32_t H[LQ];
 #pragma unroll
             for (int j = 0; j < LQ; ++j)
                 H[j] = 0u;
             uint32_t best = 0u;
-#else
-            h2 H[LQ];
-#pragma unroll
-            for (int j = 0; j < LQ; ++j)
-                H[j] = (h2){(_Float16)0.0f, (_Float16)0.0f};
-            h2 best = {(_Float16)0.0f, (_Float16)0.0f};
-#endif
             const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
             // the candidate rows arrive 16 bytes per lane per 16 DP rows (one aligned load each, the next
             // block in flight while the current one is consumed), not one byte load per row
@@ -825,37 +623,18 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 return pprof + ka * GST + kb * PST;
             };
             int i = 0;
-#if DRM_SW_ROWS == 3 && DRM_SW_INT
-            for (; i + 2 < L; i += 3) {
-                const uint32_t *p0 = row(i);
-                const uint32_t *p1 = row(i + 1);
-                const uint32_t *p2 = row(i + 2);
-                sw_row3_i16<LQ>(H, p0, p1, p2, best);
+            for (; i + DRM_SW_ROWS <= L; i += DRM_SW_ROWS) {
+                const uint32_t *pr[DRM_SW_ROWS];
+#pragma unroll
+                for (int r = 0; r < DRM_SW_ROWS; ++r)
+                    pr[r] = row(i + r); // in row order: row() steps through the candidate bytes
+                sw_rows_i16<LQ, DRM_SW_ROWS, DRM_SW_PF>(H, pr, best);
             }
-#endif
-#if DRM_SW_ROWS >= 2
-            for (; i + 1 < L; i += 2) {
-                const uint32_t *p0 = row(i);
-                const uint32_t *p1 = row(i + 1);
-#if DRM_SW_INT
-                sw_row2_i16<LQ>(H, p0, p1, best);
-#else
-                sw_row2_f16<LQ>(H, p0, p1, best);
-#endif
-            }
-#endif
             for (; i < L; ++i) {
-#if DRM_SW_INT
-                sw_row_i16<LQ>(H, row(i), best);
-#else
-                sw_row_f16<LQ>(H, row(i), best);
-#endif
+                const uint32_t *pr[1] = {row(i)};
+                sw_rows_i16<LQ, 1, DRM_SW_PF>(H, pr, best);
             }
-#if DRM_SW_INT
             const int score_a = (int)(best & 0xFFFFu), score_b = (int)(best >> 16);
-#else
-            const int score_a = (int)((float)best.x * 1024.0f), score_b = (int)((float)best.y * 1024.0f);
-#endif
             const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
             a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
             a.cand_scores[q * a.cmax + c0] = score_a;

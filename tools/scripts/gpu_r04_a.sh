@@ -13,7 +13,7 @@ for i in 1 2; do
   done
 done
 for i in 1 2; do
-  for lib in deepreadmapper_amd/libdrm_hip.so ab/sw_rows2.so; do
+  for lib in deepreadmapper_amd/libdrm_hip.so ab/sw_r2.so ab/sw_r4pf1.so ab/sw_r5pf1.so; do
     echo "== $lib"; DRM_LIB=$PWD/$lib timeout -k 10 300 python -u tools/scripts/sw_waves_probe.py --waves 0 --windows 2000000 || exit 1
   done
 done
