@@ -618,6 +618,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         else
             greedy_upper<true>(a, lut, lane, nearest, dn, ndis, nhops);
         const int nhops_upper = nhops;
+#ifdef DRM_PQ_DEBUG
+        if ((nearest < 0 || nearest >= a.ntotal) && lane == 0)
+            printf("[pq dbg] q %d: level-0 entry %d out of range\n", q, nearest);
+#endif
         DRM_FSTAMP(1);
 
         // MinimaxHeap candidates(ef); candidates.push(nearest, d_nearest)
@@ -654,6 +658,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 }, lane);
                 __builtin_amdgcn_s_waitcnt(0);
             }
+#ifdef DRM_PQ_DEBUG
+            if (logn + sn > a.log_cap && lane == 0)
+                printf("[pq dbg] q %d: log %d + %d entries past its capacity %d\n", q, logn, sn, a.log_cap);
+#endif
             if (lane < sn)
                 __hip_atomic_store(lg + logn + lane, ((uint64_t)sbh << 32) | sbl, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -734,6 +742,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if (lane == (int)((h0 >> 5) & 63u))
                     popped_bits |= 1u << (h0 & 31u);
             }
+#ifdef DRM_PQ_DEBUG
+            if (v0 < 0 || v0 >= a.ntotal) {
+                if (lane == 0)
+                    printf("[pq dbg] q %d hop %d: v0 %d out of range (nvalid %d kc %d d0 %08x)\n", q, nstep, v0, nvalid, kc, d0);
+                overrun = true;
+                break;
+            }
+#endif
             if (!hit)
                 praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
             const int32_t v1 = lane < deg0 ? (int32_t)praw.x : -1;
@@ -764,6 +780,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     pred = __builtin_amdgcn_readlane(mid, __builtin_ctzll(ballot(mk == mm)));
                     pnode = pred;
                 }
+#ifdef DRM_PQ_DEBUG
+                if (pnode < 0 || pnode >= a.ntotal) {
+                    if (lane == 0)
+                        printf("[pq dbg] q %d hop %d: predicted node %d out of range (mm %08x)\n", q, nstep, pnode, mm);
+                    pnode = v0;
+                }
+#endif
                 praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
             }
             if (STATS) {
@@ -858,6 +881,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const uint32_t T = kc == ef ? hi32(root) : 0xFFFFFFFFu;
             const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
             const int c = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) { stage[p] = e; }, lane);
+#ifdef DRM_PQ_DEBUG
+            if (c > k && lane == 0)
+                printf("[pq dbg] q %d: %d results selected from a log of %d (T %08x)\n", q, c, logn, T);
+#endif
             __syncthreads();
             {
                 uint64_t x0 = lane < c ? stage[lane] : ~0ull;
