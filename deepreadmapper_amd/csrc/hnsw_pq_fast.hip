@@ -823,6 +823,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if (kc == ef && key >= hi32(root))
                     continue;
                 const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                if (STAMPS)
+                    st_acc[4] += 1u; // links tested against the heap's ids
                 if (hp.holds(idl))
                     continue;
                 const uint64_t val = pack(key, idl);

@@ -34,8 +34,8 @@ L = lib()
 L.drm_debug_search_stamps.argtypes = [C.c_void_p, C.c_void_p]
 check(L.drm_debug_search_stamps(ix.handle, out.ctypes.data))
 if os.environ.get("DRM_SEARCH_FAST", "1") != "0":
-    names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+codes)", "distances+prefetch+clear list",
-             "push loop (+log store)", "output+clear", "queue/top", "-", "-", "row wait (hop start)", "-"]
+    names = ["lut", "greedy_upper", "pop_min+count_below", "distances+prediction+row prefetch", "-",
+             "push loop (heap-id tests, pushes, log)", "output", "queue/top", "-", "-", "row wait (hop start)", "-"]
 else:
     names = ["lut", "greedy_upper", "pop_min+count_below", "row+visited(+spec codes)", "distances+prefetch",
              "push loop: fetch/reject/overhead", "output+clear", "queue/top", "push loop: add_result",
@@ -44,7 +44,9 @@ if os.environ.get("DRM_SEARCH_FAST", "1") != "0":
     print(f"row prediction hits {int(out[8])} of {int(out[9])} hops ({out[8] / max(out[9], 1) * 100:.1f} %)")
     if out[11]:
         print(f"full-heap replace pushes {int(out[11])} ({out[11] / max(out[9], 1):.2f} per hop)")
-    out[8] = out[9] = out[11] = 0  # counts; out[10] is the hop-start row wait (time)
+    if out[4]:
+        print(f"links tested against the heap's ids {int(out[4])} ({out[4] / max(out[9], 1):.2f} per hop)")
+    out[4] = out[8] = out[9] = out[11] = 0  # counts; out[10] is the hop-start row wait (time)
 tot = float(out.sum())
 for n, v in zip(names, out):
     print(f"{n:32s} {v / tot * 100:6.2f} %")
