@@ -82,6 +82,8 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 
 void free_index(drm::DeviceIndex &d)
 {
+    if (d.trace)
+        (void)hipHostFree(d.trace);
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
                     d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes};
     for (void *p : ptrs)
@@ -267,6 +269,12 @@ int drm_index_load(const char *path, int device, drm_index **out)
                 DRM_HIP_CHECK(hipMalloc(&d.stamps, 12 * sizeof(uint64_t)));
                 DRM_HIP_CHECK(hipMemset(d.stamps, 0, 12 * sizeof(uint64_t)));
             }
+        if (const char *e = std::getenv("DRM_SEARCH_TRACE"))
+            if (std::atoi(e)) { // host memory the device writes through: readable while a kernel runs (or hangs)
+                DRM_HIP_CHECK(hipHostMalloc((void **)&d.trace, sizeof(uint32_t) * drm::kTraceWords,
+                                            hipHostMallocMapped | hipHostMallocCoherent));
+                std::memset(d.trace, 0, sizeof(uint32_t) * drm::kTraceWords);
+            }
         try {
             d.centroids = upload_vec(h.centroids, d.device_bytes);
             d.codes = upload_vec(h.codes, d.device_bytes);
@@ -313,6 +321,17 @@ int drm_debug_search_stamps(drm_index *index, uint64_t *out12)
             throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
         DRM_HIP_CHECK(hipMemcpy(out12, index->dev.stamps, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
         DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 12 * sizeof(uint64_t)));
+    });
+}
+
+// diagnostic (not part of include/drm_hip.h): the host-mapped trace of a DRM_PQ_DEBUG build (DRM_SEARCH_TRACE=1)
+int drm_debug_search_trace(drm_index *index, uint32_t **ptr, int64_t *words)
+{
+    return guarded([&] {
+        if (!index || !ptr || !words)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *ptr = index->dev.trace;
+        *words = index->dev.trace ? drm::kTraceWords : 0;
     });
 }
 

@@ -42,6 +42,7 @@ inline hipError_t malloc_big(void **p, size_t bytes, BigKind kind)
 }
 
 constexpr int kMaxLevels = 24; // HNSW levels representable in SearchArgs::cum
+constexpr int64_t kTraceWords = 8 + 8 * (1 << 20); // diagnostic trace: a count, then 8-word records
 
 // HBM image of an IndexHNSWPQ (DESIGN.md "data layout in HBM").
 struct DeviceIndex {
@@ -59,6 +60,7 @@ struct DeviceIndex {
     int32_t exact_stats = 0;   // lean kernel: count faiss's ndis with a visited bitmap (DRM_SEARCH_EXACT_STATS)
     int32_t force_lds_kernel = 0; // use the general LDS-heap kernel (hnsw_search_lds.hip)
     uint64_t *stamps = nullptr;   // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
+    uint32_t *trace = nullptr;    // diagnostic: host-mapped trace of a DRM_PQ_DEBUG build (DRM_SEARCH_TRACE=1)
     float *centroids = nullptr;    // [M][ksub][dsub] f32
     uint8_t *codes = nullptr;      // [ntotal][code_size]
     int32_t *nbr0 = nullptr;       // [ntotal][deg0] level-0 rows (128 B each at M_hnsw=16)
@@ -129,6 +131,7 @@ struct SearchArgs {
     int32_t row_words;
     const uint2 *upper_codes; // lean kernel, inline layout: codes beside upper_nbr (DeviceIndex::upper_codes)
     int32_t exact_stats;      // lean kernel: faiss's ndis counted with `visited` (else the distances computed)
+    uint32_t *trace;          // diagnostic (DRM_PQ_DEBUG builds): host-mapped records, [0] = count
 };
 
 // lean kernel (hnsw_pq_fast.hip): inline rows, PQ 8x8, level-0 degree <= 64, ef <= 128, k == ef or k <= 64

@@ -547,6 +547,31 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     return cnt;
 }
 
+#ifdef DRM_PQ_DEBUG
+// diagnostic trace (DRM_PQ_DEBUG builds, DRM_SEARCH_TRACE=1): lane 0 appends an 8-word record to host memory, which
+// the host can read while the kernel runs -- or hangs
+__device__ void dbg_rec(const SearchArgs &a, uint32_t tag, int q, int hop, uint32_t w3, uint32_t w4, uint32_t w5,
+                        uint32_t w6, uint32_t w7)
+{
+    if (!a.trace)
+        return;
+    const uint32_t i = __hip_atomic_fetch_add(a.trace, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((int64_t)i * 8 + 16 > kTraceWords)
+        return;
+    uint32_t *r = a.trace + 8 + (size_t)i * 8;
+    const uint32_t v[8] = {tag, (uint32_t)q, (uint32_t)hop, w3, w4, w5, w6, w7};
+    for (int j = 0; j < 8; ++j)
+        __hip_atomic_store(r + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define DRM_DBG(...)                                                                                         \
+    do {                                                                                                    \
+        if (lane == 0)                                                                                      \
+            dbg_rec(a, __VA_ARGS__);                                                                        \
+    } while (0)
+#else
+#define DRM_DBG(...) do {} while (0)
+#endif
+
 #define DRM_FSTAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -682,6 +707,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (a.clear_cap > 0)
                 clr[0] = nearest;
         }
+        DRM_DBG(1u, q, 0, (uint32_t)nearest, dn, (uint32_t)ef, (uint32_t)k, (uint32_t)ef_search);
         int nstep = 0, ndis0 = 0;
         bool overrun = false;
         int32_t pred = -1;
@@ -724,6 +750,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (wl == 63 && wR)
                 root = (root & ~0xFFFFFFFFull) | kPopLo;
             nvalid--;
+            DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)nvalid, (uint32_t)kc, hi32(root));
             // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
             const int below = __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
             if (below >= ef_search)
@@ -758,6 +785,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const int jmax = negm ? __builtin_ctzll(negm) : 64; // lanes past deg0 hold -1
             const uint64_t actm = negm ? (negm & (0ull - negm)) - 1ull : ~0ull;
             DRM_FSTAMP(10);
+            DRM_DBG(3u, q, nstep, (uint32_t)jmax, (uint32_t)pred, (uint32_t)hit, (uint32_t)__builtin_amdgcn_readfirstlane(v1),
+                    (uint32_t)logn);
             // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min: the
             // smallest valid heap slot or link not known to be popped; its row is fetched now and waited for at
             // the next hop
@@ -828,6 +857,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if (hp.holds(idl))
                     continue;
                 const uint64_t val = pack(key, idl);
+                DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
                 if (!LOGRES) {
                     if (key < thr)
                         add_result(val);
@@ -910,6 +940,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             a.D[o] = valid ? unord32(hi32(rv)) : INFINITY;
             a.I[o] = valid ? (int64_t)unpack_id(rv) : (int64_t)-1;
         }
+        DRM_DBG(5u, q, nstep, (uint32_t)logn, (uint32_t)overrun, (uint32_t)kc, hi32(root), 0u);
         if (lane == 0) {
             a.ndis[q] = overrun ? -1 : ndis + ndis0;
             a.nhops[q] = overrun ? -1 : nhops + nstep;

@@ -1160,6 +1160,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.counter = ix.counter;
     a.check_dups = ix.has_dup_links;
     a.stamps = ix.stamps;
+    a.trace = ix.trace;
     a.x_aligned16 = ((uintptr_t)d_x % 16) == 0;
 
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
