@@ -140,10 +140,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     for (;;) {
-        int qi = 0;
-        if (lane == 0)
-            qi = (int)atomicAdd(a.counter, 1u);
-        qi = __builtin_amdgcn_readfirstlane(qi);
+        const int qi = wave_next_item(a.counter, lane);
         if ((int64_t)qi >= a.count)
             break;
         const int32_t u = a.order[a.start + qi];

@@ -337,3 +337,18 @@ void launch_tokenize(const DeviceEncoder &d, const uint8_t *d_seqs, const int32_
                      int32_t *d_tokens, hipStream_t stream);
 
 } // namespace drm
+
+#if defined(__HIP__)
+namespace drm {
+// The wave's next item from a persistent kernel's atomic work queue (counter[0]). Every lane executes the atomic
+// (lane 0 adds 1, the others 0) and the wave takes lane 0's old value: no branch on the lane id sits in front of the
+// readfirstlane. With the usual `if (lane == 0) q = atomicAdd(..)` a search kernel whose loop body also ends in
+// `if (lane == 0)` stores was compiled into two loops split on the lane id (lane 0 left to fetch the next item,
+// lanes 1..63 looped back with q = 0 and re-ran item 0 forever): a hang, seen in round 4.
+__device__ __forceinline__ int wave_next_item(uint32_t *counter, int lane)
+{
+    const uint32_t old = __hip_atomic_fetch_add(counter, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane((int)old);
+}
+} // namespace drm
+#endif

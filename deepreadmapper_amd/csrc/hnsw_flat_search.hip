@@ -701,10 +701,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
     const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
 
     for (;;) {
-        int qi = 0;
-        if (lane == 0)
-            qi = (int)atomicAdd(a.counter, 1u);
-        qi = __builtin_amdgcn_readfirstlane(qi);
+        int qi = wave_next_item(a.counter, lane);
         if ((int64_t)qi >= nq)
             break;
         if (a.qlist)

@@ -547,10 +547,10 @@ __device__ __forceinline__ int log_select(const uint64_t *lg, int logn, uint32_t
     return cnt;
 }
 
-#ifdef DRM_PQ_DEBUG
-// diagnostic trace (DRM_PQ_DEBUG builds, DRM_SEARCH_TRACE=1): lane 0 appends an 8-word record to host memory, which
+#ifdef DRM_PQ_TRACE
+// diagnostic trace (DRM_PQ_TRACE builds, DRM_SEARCH_TRACE=1): lane 0 appends an 8-word record to host memory, which
 // the host can read while the kernel runs -- or hangs
-__device__ void dbg_rec(const SearchArgs &a, uint32_t tag, int q, int hop, uint32_t w3, uint32_t w4, uint32_t w5,
+__device__ __forceinline__ void dbg_rec(const SearchArgs &a, uint32_t tag, int q, int hop, uint32_t w3, uint32_t w4, uint32_t w5,
                         uint32_t w6, uint32_t w7)
 {
     if (!a.trace)
@@ -563,13 +563,20 @@ __device__ void dbg_rec(const SearchArgs &a, uint32_t tag, int q, int hop, uint3
     for (int j = 0; j < 8; ++j)
         __hip_atomic_store(r + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-#define DRM_DBG(...)                                                                                         \
+// written by the first active lane; the tag word carries the active lane count (bits 16..23) and that lane (24..31),
+// so a record made with part of the wave masked off shows it
+#define DRM_DBG(tag, ...)                                                                                    \
     do {                                                                                                    \
-        if (lane == 0)                                                                                      \
-            dbg_rec(a, __VA_ARGS__);                                                                        \
+        const uint64_t _ex = __builtin_amdgcn_read_exec();                                                  \
+        if (lane == __builtin_ctzll(_ex))                                                                   \
+            dbg_rec(a, (tag) | ((uint32_t)__builtin_popcountll(_ex) << 16) | ((uint32_t)lane << 24), __VA_ARGS__); \
     } while (0)
 #else
 #define DRM_DBG(...) do {} while (0)
+#endif
+
+#ifndef DRM_PQ_BISECT
+#define DRM_PQ_BISECT 0 // diagnostic builds only: 1 no heap-id test, 3 no hop bound, 4 no row prefetch
 #endif
 
 #define DRM_FSTAMP(idx)                                                                                     \
@@ -610,10 +617,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     const uint32_t kInfKey = ord32(INFINITY);
 
     for (;;) {
-        int q = 0;
-        if (lane == 0)
-            q = (int)atomicAdd(a.counter, 1u);
-        q = __builtin_amdgcn_readfirstlane(q);
+        const int q = wave_next_item(a.counter, lane);
+        DRM_DBG(16u, q, 0, (uint32_t)a.n, 0u, 0u, 0u, 0u);
         if ((int64_t)q >= a.n)
             break;
         if (a.entry_point < 0 || a.ntotal == 0) {
@@ -720,10 +725,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
             // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the
             // bookkeeping is broken -- end the query with an error status rather than loop
+#if DRM_PQ_BISECT != 3
             if (nstep > a.ntotal) {
                 overrun = true;
                 break;
             }
+#endif
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
@@ -816,7 +823,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     pnode = v0;
                 }
 #endif
+#if DRM_PQ_BISECT == 4
+                pred = -1;
+#else
                 praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
+#endif
             }
             if (STATS) {
                 // VisitedTable get + set of every link, in row order (lanes of one atomic instruction that share a
@@ -854,8 +865,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const int32_t idl = __builtin_amdgcn_readlane(v1, l);
                 if (STAMPS)
                     st_acc[4] += 1u; // links tested against the heap's ids
+#if DRM_PQ_BISECT != 1
                 if (hp.holds(idl))
                     continue;
+#endif
                 const uint64_t val = pack(key, idl);
                 DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
                 if (!LOGRES) {
@@ -905,35 +918,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         DRM_FSTAMP(2);
 
         // --- SingleResultHandler::end (heap_reorder): ascending (distance, id), (+inf, -1) padding
+        DRM_DBG(6u, q, nstep, (uint32_t)(uintptr_t)lg, (uint32_t)((uintptr_t)lg >> 32), (uint32_t)a.log_cap,
+                (uint32_t)sn, (uint32_t)logn);
         if (LOGRES) {
             if (sn)
                 log_flush();
+            DRM_DBG(7u, q, nstep, (uint32_t)logn, 0u, 0u, 0u, 0u);
             __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
+            DRM_DBG(8u, q, nstep, 0u, 0u, 0u, 0u, 0u);
             __syncthreads();
             const uint32_t T = kc == ef ? hi32(root) : 0xFFFFFFFFu;
             const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
+            DRM_DBG(9u, q, nstep, T, idthr, 0u, 0u, 0u);
             const int c = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) { stage[p] = e; }, lane);
+            DRM_DBG(10u, q, nstep, (uint32_t)c, 0u, 0u, 0u, 0u);
 #ifdef DRM_PQ_DEBUG
             if (c > k && lane == 0)
                 printf("[pq dbg] q %d: %d results selected from a log of %d (T %08x)\n", q, c, logn, T);
 #endif
             __syncthreads();
+            DRM_DBG(11u, q, nstep, 0u, 0u, 0u, 0u, 0u);
             {
                 uint64_t x0 = lane < c ? stage[lane] : ~0ull;
                 uint64_t x1 = lane + 64 < c ? stage[lane + 64] : ~0ull;
                 sort128(x0, x1, lane);
+                DRM_DBG(12u, q, nstep, 0u, 0u, 0u, 0u, 0u);
                 __syncthreads();
                 stage[lane] = x0;
                 stage[lane + 64] = x1;
                 __syncthreads();
             }
+            DRM_DBG(13u, q, nstep, (uint32_t)(uintptr_t)a.D, (uint32_t)((uintptr_t)a.D >> 32), (uint32_t)(uintptr_t)a.I,
+                    (uint32_t)((uintptr_t)a.I >> 32), (uint32_t)k);
+#ifndef DRM_PQ_DEBUG_NO_OUT
             for (int j = lane; j < k; j += 64) {
                 const int64_t o = (int64_t)q * k + j;
                 const uint64_t e = stage[j];
                 a.D[o] = j < c ? unord32(hi32(e)) : INFINITY;
                 a.I[o] = j < c ? (int64_t)unpack_id(e) : (int64_t)-1;
             }
+#endif
+            DRM_DBG(14u, q, nstep, 0u, 0u, 0u, 0u, 0u);
+#ifndef DRM_PQ_DEBUG_NO_BAR
             __syncthreads();
+#endif
+            DRM_DBG(15u, q, nstep, 0u, 0u, 0u, 0u, 0u);
         } else if (lane < k) {
             const int64_t o = (int64_t)q * k + lane;
             const bool valid = rv != ~0ull;
@@ -949,6 +978,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (overrun)
                 atomicAdd(a.counter + 3, 1u);
         }
+        DRM_DBG(18u, q, nstep, 0u, 0u, 0u, 0u, 0u);
         if (STATS) { // VisitedTable::advance: clear exactly the bits this query set; they land before the next query
             if (clear_n <= a.clear_cap) {
                 for (int t = lane; t < clear_n; t += 64)
@@ -962,6 +992,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         }
         DRM_FSTAMP(6);
     }
+    DRM_DBG(17u, 0, 0, 0u, 0u, 0u, 0u, 0u);
     if (STAMPS && lane == 0 && a.stamps)
         for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);

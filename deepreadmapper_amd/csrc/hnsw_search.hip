@@ -410,10 +410,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
 
     for (;;) {
-        int q = 0;
-        if (lane == 0)
-            q = (int)atomicAdd(a.counter, 1u);
-        q = __builtin_amdgcn_readfirstlane(q);
+        int q = wave_next_item(a.counter, lane);
         if ((int64_t)q >= nq)
             break;
         if (a.qlist)
@@ -788,10 +785,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     constexpr uint32_t kPopped = 0x80000000u;
 
     for (;;) {
-        int q = 0;
-        if (lane == 0)
-            q = (int)atomicAdd(a.counter, 1u);
-        q = __builtin_amdgcn_readfirstlane(q);
+        const int q = wave_next_item(a.counter, lane);
         if ((int64_t)q >= a.n)
             break;
 

@@ -187,10 +187,7 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_lds_kernel(SearchArgs a)
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
 
     for (;;) {
-        int64_t q = 0;
-        if (lane == 0)
-            q = (int64_t)atomicAdd(a.counter, 1u);
-        q = (int64_t)__builtin_amdgcn_readfirstlane((int)q);
+        const int64_t q = wave_next_item(a.counter, lane);
         if (q >= a.n)
             break;
 

@@ -323,6 +323,7 @@ def test_search_device_stats(syn20k):
     w = syn20k["w"]
     q = w.q_emb[:500]
     ix = read_index(syn20k["index"])
+    ix.set_exact_stats(True)  # ndis as faiss counts it (the default mode reports the distances computed)
     dq = DeviceBuffer.from_host(q)
     dD, dI = DeviceBuffer((500, 128), np.float32), DeviceBuffer((500, 128), np.int64)
     nd, nh = DeviceBuffer(500, np.int32), DeviceBuffer(500, np.int32)
