@@ -87,7 +87,7 @@ struct DeviceIndex {
     int32_t use_fast = 1;          // lean kernel (hnsw_pq_fast.hip) where it applies; DRM_SEARCH_FAST=0 off
     uint64_t *log = nullptr;       // [n_slots][log_cap] accepted pushes (lean kernel, k == ef)
     int32_t log_cap = 0, log_slots = 0;
-    int32_t log_cap_req = 2048;    // entries per slot (DRM_SEARCH_LOG_CAP; >= ef + 64, compaction beyond)
+    int32_t log_cap_req = 512;     // entries per slot (DRM_SEARCH_LOG_CAP; >= ef + max(ef, 64), compaction beyond)
     // the lean kernel keeps no visited table (its heap is the visited set): the bitmap above
     // is allocated only for the other kernels, or for exact_stats
     int64_t device_bytes = 0;

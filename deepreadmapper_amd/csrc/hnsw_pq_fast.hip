@@ -133,13 +133,13 @@ struct PathConst {
     uint32_t Alo, Auplo, Lreqlo;
     // ds_bpermute byte addresses: this lane's left / right child lane (slots 2p+1, 2p+2 are held by lanes
     // 2p+1, 2p+2 mod 64), and its parent in the chain of slot 127's ancestors (lane >> 1)
-    uint32_t addrL, addrR, addrHalf;
+    uint32_t addrL, addrR, addrHalf, half; // half = lane >> 1
     // heap filling (push_fill): this lane's slots 2p+1, 2p+2 as 1-based positions 2p+2, 2p+3 share the bit
     // length bl; their father is slot p, held by lane (p-1)/2 (the L half when p is odd; the root for p = 0)
     uint32_t c2, bl, addrF;
     __device__ explicit PathConst(int lane)
         : addrL((uint32_t)((2 * lane + 1) & 63) << 2), addrR((uint32_t)((2 * lane + 2) & 63) << 2),
-          addrHalf((uint32_t)(lane >> 1) << 2), c2(2u * (uint32_t)lane + 2u), bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)),
+          addrHalf((uint32_t)(lane >> 1) << 2), half((uint32_t)lane >> 1), c2(2u * (uint32_t)lane + 2u), bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)),
           addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 0u)
     {
         uint64_t A = 1ull << lane, Aup = 0, Lreq = 0;
@@ -284,14 +284,14 @@ struct Heap {
     //    of lanes 31, 15, 7, 3, 1, 0; then the root). Chain holder c takes its father, slot c, whose post-pop value
     //    is lane c's own chv (or slot 127's value) if lane c >> 1 is on the path and took its L child, else its
     //    pre-pop value: the only cross-lane part is the pre-pop fetch.
-    // The root (slot 0) lives in scalar registers (root, rootI) during a row's pushes: lane 63's R key is left
-    // stale here and refreshed by the hop; returns the root after the push, its id in rootI.
-    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int lane,
-                                                   int32_t &rootI)
+    // Straight-line: every case is a lane mask (no branch), and lane 63's R (the root) is current on return. Returns
+    // the root after the push, its id in rootI.
+    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int32_t &rootI)
     {
+        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const uint64_t val = readlane64(L, 63); // slot 127
         const int32_t valI = readlane32(IL, 63);
-        const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child
+        const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child (node 63: slot 127 only)
         const bool takeL = in_mask(lm);
         const uint64_t chv = takeL ? L : R;
         const int32_t chI = takeL ? IL : IR;
@@ -302,62 +302,57 @@ struct Heap {
         const int32_t fpreI = bperm32_addr(IL, pc.addrHalf);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
-        uint64_t rootv = val;
-        int32_t rI = valI;
-        uint32_t last = 64u;
-        if (W) {
-            last = 63u - (uint32_t)__builtin_clzll(W);
-            const bool atlast = in_mask(1ull << last);
-            const uint64_t up = atlast ? val : up0;
-            const int32_t upI = atlast ? valI : up0I;
-            const bool wl = in_mask(W & lm), wr = in_mask(W & ~lm);
-            L = wl ? up : L;
-            IL = wl ? upI : IL;
-            R = wr ? up : R;
-            IR = wr ? upI : IR;
-            if (W & 1ull) {
-                rootv = readlane64(chv, 0);
-                rI = readlane32(chI, 0);
-            }
-        }
-        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
-        constexpr uint64_t kAncL = kHold & ~(1ull << 63);
-        const int h = __builtin_popcountll(ballot(vnew > L) & kAncL) + (sgt64(vnew, rootv) ? 1 : 0);
-        if (h == 0) {
-            const bool s127 = in_mask(1ull << 63);
-            L = s127 ? vnew : L;
-            IL = s127 ? vnewI : IL;
-            rootI = rI;
-            return rootv;
-        }
-        const uint32_t k = (uint32_t)lane >> 1;
-        const bool moved = (((W & lm) >> k) & 1ull) != 0ull;
-        const bool klast = k == last;
-        const uint64_t fl = moved ? (klast ? val : chv) : fpre;
-        const int32_t flI = moved ? (klast ? valI : chI) : fpreI;
-        const bool wm = in_mask(kHold & (~0ull << ((1u << (7 - h)) - 1u))); // chain index < h
-        L = wm ? fl : L;
-        IL = wm ? flI : IL;
-        if (h == 7) { // vnew becomes the root; the old root moves down to slot 1 (lane 0)
-            const bool s1 = in_mask(1ull);
-            L = s1 ? rootv : L;
-            IL = s1 ? rI : IL;
-            rootI = vnewI;
-            return vnew;
-        }
-        const bool sx = in_mask(1ull << ((1u << (6 - h)) - 1u)); // the chain slot at index h
-        L = sx ? vnew : L;
-        IL = sx ? vnewI : IL;
-        rootI = rI;
-        return rootv;
+        const int last = 63 - __builtin_clzll(W | 1ull); // the path's deepest node (read only under W)
+        const uint64_t c0 = readlane64(chv, 0);
+        const int32_t c0I = readlane32(chI, 0);
+        const bool r0 = (W & 1ull) != 0ull; // the root's larger child moves up
+        const uint64_t rootv = r0 ? c0 : val;
+        const int32_t rI = r0 ? c0I : valI;
+        // pop writes: the path nodes' chosen child slots
+        const bool atlast = in_mask(1ull << last);
+        const uint64_t up = atlast ? val : up0;
+        const int32_t upI = atlast ? valI : up0I;
+        const uint64_t wlm = W & lm;
+        // the chain's fathers after the pop (lane 0's is the root)
+        const bool moved = (((uint32_t)wlm >> pc.half) & 1u) != 0u;
+        const bool klast = pc.half == (uint32_t)last;
+        uint64_t fl = moved ? (klast ? val : chv) : fpre;
+        int32_t flI = moved ? (klast ? valI : chI) : fpreI;
+        const bool wl = in_mask(wlm), wr = in_mask(W & ~lm);
+        L = wl ? up : L;
+        IL = wl ? upI : IL;
+        R = wr ? up : R;
+        IR = wr ? upI : IR;
+        // push: h = the chain's ancestors below vnew after the pop (lane 63 stands for the root)
+        const bool s63 = in_mask(1ull << 63);
+        const uint64_t chain = s63 ? rootv : L;
+        const int h = __builtin_popcountll(ballot(vnew > chain) & kHold);
+        const bool s1 = in_mask(1ull);
+        fl = s1 ? rootv : fl;
+        flI = s1 ? rI : flI;
+        // chain index m (slot 127 = 0, 63 = 1, ..., 1 = 6; the root = 7) is lane (1 << (6 - m)) - 1's L half: the
+        // indices below h take their father's value, index h takes vnew
+        const uint64_t shm = h ? kHold & (~0ull << ((1u << (7 - h)) - 1u)) : 0ull;
+        const bool sh = in_mask(shm);
+        L = sh ? fl : L;
+        IL = sh ? flI : IL;
+        const uint64_t xm = h < 7 ? 1ull << ((1u << (6 - h)) - 1u) : 0ull;
+        const bool xs = in_mask(xm);
+        L = xs ? vnew : L;
+        IL = xs ? vnewI : IL;
+        const uint64_t nroot = h == 7 ? vnew : rootv;
+        rootI = h == 7 ? vnewI : rI;
+        R = s63 ? nroot : R;
+        IR = s63 ? rootI : IR;
+        return nroot;
     }
 
     // faiss heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128): val enters slot s = k - 1 and
     // sifts up its ancestors, slot (k >> m) - 1 at chain index m (the root at m = bitlen(k) - 1). Lane-mask
     // form: each lane tests whether one of its halves is on the chain (both halves share the index), the
     // ancestors below val are a bottom prefix of length h (heap order), the slots of index < h take their
-    // father's value (one ds_bpermute per half), and the slot of index h takes val. The root is (rootv, rootI)
-    // (scalar; lane 63's R key is left stale); returns the new root, its id in rootI.
+    // father's value (one ds_bpermute per half), and the slot of index h takes val. The root is (rootv, rootI),
+    // also in lane 63's R / IR; returns the new root, its id in rootI.
     __device__ __forceinline__ uint64_t push_fill(int k, uint64_t val, int32_t valI, const PathConst &pc, uint64_t rootv,
                                                   int32_t &rootI)
     {
@@ -389,6 +384,9 @@ struct Heap {
                 R = rr ? rootv : R;
                 IR = rr ? rootI : IR;
                 rootI = valI;
+                const bool s63 = in_mask(1ull << 63);
+                R = s63 ? val : R;
+                IR = s63 ? valI : IR;
                 return val;
             }
         }
@@ -575,10 +573,6 @@ __device__ __forceinline__ void dbg_rec(const SearchArgs &a, uint32_t tag, int q
 #define DRM_DBG(...) do {} while (0)
 #endif
 
-#ifndef DRM_PQ_BISECT
-#define DRM_PQ_BISECT 0 // diagnostic builds only: 1 no heap-id test, 3 no hop bound, 4 no row prefetch
-#endif
-
 #define DRM_FSTAMP(idx)                                                                                     \
     do {                                                                                                    \
         if (STAMPS) {                                                                                       \
@@ -673,21 +667,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             rv = lane > pos ? sh : (lane == pos ? v : rv);
             thr = (uint32_t)__builtin_amdgcn_readlane((int)hi32(rv), k - 1);
         };
-        // accepted pushes not yet stored (k == ef): lanes [0, sn) of (sbh, sbl) = (key, id ^ 2^31) in log order
+        // k == ef: the result set is the heap's entries (with their node ids) plus the log of evicted entries that
+        // tied with the root left behind. Evictions not yet stored: lanes [0, sn) of (sbh, sbl) =
+        // (key, id ^ 2^31)
         uint32_t sbh = 0u, sbl = 0u;
         int sn = 0;
-        // compacts the stored log to the current k results when the staged entries would overflow it (T = the heap
-        // root's key: the k-th smallest of every accepted push so far, stored or staged, so no entry of the final
-        // result set is dropped), then appends the staged entries
+        // compacts the stored log when the staged entries would overflow it -- every logged entry is at or above the
+        // root, and only those at the root's distance can still be results: k of them, the smallest ids, are kept
+        // (T = the root's key) -- then appends the staged entries
+        auto log_compact = [&]() {
+            const uint32_t T = hi32(root);
+            const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
+            logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
+                __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }, lane);
+            __builtin_amdgcn_s_waitcnt(0);
+        };
         auto log_flush = [&]() {
-            if (logn + sn > a.log_cap) {
-                const uint32_t T = hi32(root);
-                const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
-                logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
-                    __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }, lane);
-                __builtin_amdgcn_s_waitcnt(0);
-            }
+            if (logn + sn > a.log_cap)
+                log_compact();
 #ifdef DRM_PQ_DEBUG
             if (logn + sn > a.log_cap && lane == 0)
                 printf("[pq dbg] q %d: log %d + %d entries past its capacity %d\n", q, logn, sn, a.log_cap);
@@ -698,11 +696,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             logn += sn;
             sn = 0;
         };
-        if (LOGRES) {
-            if (lane == 0)
-                lg[0] = root;
-            logn = 1;
-        } else {
+        if (!LOGRES) {
             if (dn < thr)
                 add_result(root);
         }
@@ -725,12 +719,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
             // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the
             // bookkeeping is broken -- end the query with an error status rather than loop
-#if DRM_PQ_BISECT != 3
             if (nstep > a.ntotal) {
                 overrun = true;
                 break;
             }
-#endif
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
@@ -823,11 +815,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     pnode = v0;
                 }
 #endif
-#if DRM_PQ_BISECT == 4
-                pred = -1;
-#else
                 praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
-#endif
             }
             if (STATS) {
                 // VisitedTable get + set of every link, in row order (lanes of one atomic instruction that share a
@@ -853,65 +841,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // below the root was seen iff it is in the heap (popped or not): a seen link either entered the heap
             // and is still there, or was rejected / evicted at a root that is now at or below its distance.
             uint64_t rem = actm;
-            if (kc == ef)
-                rem &= ballot(dall < hi32(root));
-            bool replaced = false;
-            while (rem) {
-                const int l = __builtin_ctzll(rem);
-                rem &= rem - 1;
-                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
-                if (kc == ef && key >= hi32(root))
-                    continue;
-                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
-                if (STAMPS)
-                    st_acc[4] += 1u; // links tested against the heap's ids
-#if DRM_PQ_BISECT != 1
-                if (hp.holds(idl))
-                    continue;
-#endif
-                const uint64_t val = pack(key, idl);
-                DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
-                if (!LOGRES) {
-                    if (key < thr)
+            if (kc < ef) { // the heap fills: every link not in it is pushed
+                while (rem && kc < ef) {
+                    const int l = __builtin_ctzll(rem);
+                    rem &= rem - 1;
+                    const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
+                    const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                    if (STAMPS)
+                        st_acc[4] += 1u; // links tested against the heap's ids
+                    if (hp.holds(idl))
+                        continue;
+                    const uint64_t val = pack(key, idl);
+                    DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
+                    if (!LOGRES && key < thr)
                         add_result(val);
-                }
-                if (kc == ef) { // MinimaxHeap::push on a full heap: pop the max, push val
-                    if (lo32(root) != kPopLo)
-                        --nvalid;
-                    if (ef == 128) {
-                        root = hp.replace128(val, idl, pconst, lane, rootI);
-                        hp.IR = in_mask(1ull << 63) ? rootI : hp.IR;
-                        replaced = true;
-                        if (STAMPS)
-                            st_acc[11] += 1u;
-                    } else {
-                        hp.pop(kc, lane);
-                        hp.push(kc, val, idl, lane);
-                        root = readlane64(hp.R, 63);
-                    }
-                } else {
                     ++kc;
                     if (ef == 128) {
                         root = hp.push_fill(kc, val, idl, pconst, root, rootI);
-                        hp.IR = in_mask(1ull << 63) ? rootI : hp.IR;
-                        replaced = true;
                     } else {
                         hp.push(kc, val, idl, lane);
                         root = readlane64(hp.R, 63);
+                        rootI = readlane32(hp.IR, 63);
                     }
+                    ++nvalid;
                 }
-                ++nvalid;
-                if (LOGRES) {
+                if (kc == ef)
+                    rem &= ballot(dall < hi32(root));
+            } else {
+                rem &= ballot(dall < hi32(root));
+            }
+            while (rem) { // MinimaxHeap::push on the full heap: pop the max, push val
+                const int l = __builtin_ctzll(rem);
+                rem &= rem - 1;
+                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
+                if (key >= hi32(root))
+                    continue;
+                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                if (STAMPS)
+                    st_acc[4] += 1u;
+                if (hp.holds(idl))
+                    continue;
+                const uint64_t val = pack(key, idl);
+                DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
+                if (!LOGRES && key < thr)
+                    add_result(val);
+                const uint32_t evk = hi32(root); // the evicted slot: the root (its node id in rootI)
+                const int32_t evi = rootI;
+                nvalid += lo32(root) == kPopLo ? 1 : 0; // --nvalid unless the evicted slot was popped; ++nvalid
+                if (ef == 128) {
+                    root = hp.replace128(val, idl, pconst, rootI);
+                    if (STAMPS)
+                        st_acc[11] += 1u;
+                } else {
+                    hp.pop(kc, lane);
+                    hp.push(kc, val, idl, lane);
+                    root = readlane64(hp.R, 63);
+                    rootI = readlane32(hp.IR, 63);
+                }
+                // LOGRES: an evicted result at the new root's distance can still be among the k results (the result
+                // handler breaks distance ties by node id, the MinimaxHeap by slot); any other evicted one cannot
+                if (LOGRES && evk == hi32(root)) {
                     if (sn == 64)
                         log_flush();
                     const bool at = lane == sn; // lane sn takes the entry (one compare, two selects)
-                    sbh = at ? key : sbh;
-                    sbl = at ? lo32(val) : sbl;
+                    sbh = at ? evk : sbh;
+                    sbl = at ? (uint32_t)evi ^ 0x80000000u : sbl;
                     ++sn;
                 }
             }
-            if (replaced && lane == 63) // the ef = 128 pushes kept the root in scalars
-                hp.R = root;
             nstep++;
             DRM_FSTAMP(5);
         }
@@ -923,6 +920,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         if (LOGRES) {
             if (sn)
                 log_flush();
+            // the heap's entries join the log, with their node ids (slots never filled are left out); room for them:
+            // a compacted log holds at most k entries, and log_cap >= k + ef (host side)
+            if (logn + kc > a.log_cap)
+                log_compact();
+            {
+                const bool hl = hp.IL >= 0, hr = hp.IR >= 0;
+                const uint64_t mL = ballot(hl), mR = ballot(hr), below = lanes_below(lane);
+                if (hl)
+                    __hip_atomic_store(lg + logn + __builtin_popcountll(mL & below), pack(hi32(hp.L), hp.IL),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (hr)
+                    __hip_atomic_store(lg + logn + __builtin_popcountll(mL) + __builtin_popcountll(mR & below),
+                                       pack(hi32(hp.R), hp.IR), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef DRM_PQ_DEBUG
+                if (__builtin_popcountll(mL) + __builtin_popcountll(mR) != kc && lane == 0)
+                    printf("[pq dbg] q %d: %d heap slots hold an id, %d filled\n", q,
+                           __builtin_popcountll(mL) + __builtin_popcountll(mR), kc);
+#endif
+                logn += __builtin_popcountll(mL) + __builtin_popcountll(mR);
+            }
             DRM_DBG(7u, q, nstep, (uint32_t)logn, 0u, 0u, 0u, 0u);
             __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
             DRM_DBG(8u, q, nstep, 0u, 0u, 0u, 0u, 0u);
@@ -950,18 +967,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             DRM_DBG(13u, q, nstep, (uint32_t)(uintptr_t)a.D, (uint32_t)((uintptr_t)a.D >> 32), (uint32_t)(uintptr_t)a.I,
                     (uint32_t)((uintptr_t)a.I >> 32), (uint32_t)k);
-#ifndef DRM_PQ_DEBUG_NO_OUT
             for (int j = lane; j < k; j += 64) {
                 const int64_t o = (int64_t)q * k + j;
                 const uint64_t e = stage[j];
                 a.D[o] = j < c ? unord32(hi32(e)) : INFINITY;
                 a.I[o] = j < c ? (int64_t)unpack_id(e) : (int64_t)-1;
             }
-#endif
             DRM_DBG(14u, q, nstep, 0u, 0u, 0u, 0u, 0u);
-#ifndef DRM_PQ_DEBUG_NO_BAR
             __syncthreads();
-#endif
             DRM_DBG(15u, q, nstep, 0u, 0u, 0u, 0u, 0u);
         } else if (lane < k) {
             const int64_t o = (int64_t)q * k + lane;

@@ -1029,7 +1029,7 @@ void reserve_search_scratch(DeviceIndex &ix)
     }
     DRM_HIP_CHECK(hipMalloc(&ix.counter, 4 * sizeof(uint32_t)));
     DRM_HIP_CHECK(hipMemset(ix.counter, 0, 4 * sizeof(uint32_t)));
-    const int cap = std::max(ix.log_cap_req, 128 + 64); // what the lean kernel asks for at ef = 128
+    const int cap = std::max(ix.log_cap_req, 128 + 128); // what the lean kernel asks for at ef = 128
     if (ix.log)
         DRM_HIP_CHECK(hipFree(ix.log));
     DRM_HIP_CHECK(hipMalloc(&ix.log, sizeof(uint64_t) * (size_t)slots * (size_t)cap));
@@ -1160,7 +1160,8 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
     if (fast_path) {
         // the lean kernel (hnsw_pq_fast.hip); k == ef logs accepted pushes per slot
-        const int cap = std::max(ix.log_cap_req, efc + 64); // one hop appends <= 64 after a compaction
+        // a compacted log holds <= k <= ef entries; then up to 64 staged evictions, or the ef heap entries at the end
+        const int cap = std::max(ix.log_cap_req, efc + std::max(efc, 64));
         const int need = std::max(ix.log_slots, slots);
         if (!ix.log || ix.log_cap != cap || ix.log_slots < need) {
             if (ix.log) {

@@ -364,7 +364,7 @@ constexpr int kNeedBitProfile = -4;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 #ifndef DRM_SW_ROWS
-#define DRM_SW_ROWS 3 // DP rows in flight per pass over the columns (sw_rows_i16)
+#define DRM_SW_ROWS 2 // DP rows in flight per pass over the columns (sw_rows_i16); 2 measured fastest of 2-5
 #endif
 #ifndef DRM_SW_PF
 #define DRM_SW_PF 2 // profile groups (4 columns each) read ahead of the one in use, per row

@@ -295,9 +295,9 @@ def test_search_lean_and_exact_kernels_ties(repeats, k, ef, fast, monkeypatch):
 
 
 def test_search_lean_kernel_log_compaction(syn20k, repeats, monkeypatch):
-    """A log capacity just above ef forces the in-place compaction of the accepted-push log
-    (the result set is re-derived mid-walk) on most queries: still bit-identical."""
-    monkeypatch.setenv("DRM_SEARCH_LOG_CAP", "1")  # clamped to ef + 64
+    """The smallest log capacity (ef + max(ef, 64)) forces the in-place compaction of the log of tied
+    evictions on the tie-heavy index (and before the heap's entries join it at the end): still bit-identical."""
+    monkeypatch.setenv("DRM_SEARCH_LOG_CAP", "1")  # clamped to ef + max(ef, 64)
     w = syn20k["w"]
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb[:600], 128, 128)
     _search_both(repeats["index"], repeats["fx"], repeats["q"], 96, 96)

@@ -1,8 +1,8 @@
 """Host models of the lean search kernel (tools/emu/): its wave-parallel MinimaxHeap with node ids
 (Heap::replace128 / push_fill, pop_min's slot marking, Heap::holds) against a literal faiss MinimaxHeap under
-random pushes and pops with many equal distances, and its level-0 loop -- the heap as the visited set -- over the
-committed C1 fixture, which must give the committed rows with no node pushed twice and the push log within its
-capacity. CPU only: each lane of the wave is a loop index."""
+random pushes and pops with many equal distances, and its level-0 loop -- the heap as the visited set, the log of
+tied evictions, the result set from the heap plus that log -- over the committed C1 fixture, which must give the
+committed rows with no node pushed twice and the log within its capacity. CPU only: each lane of the wave is a loop index."""
 import ctypes as C
 import os
 import subprocess

@@ -72,12 +72,12 @@ int main(int argc, char **argv)
             } else if (kc == n) {
                 if (key >= hi32(root)) { if (ok_ref) { std::printf("trial %d: reject mismatch\n", t); std::exit(1); } return; }
                 if (n == 128) {
-                    root = hp.replace128(pack(key, id), id, pc, rootI); hp.R[63] = root; hp.IR[63] = rootI;
+                    root = hp.replace128(pack(key, id), id, pc, rootI);
                 } else {
                     hp.pop(kc); hp.push(kc, pack(key, id), id); root = hp.R[63]; rootI = hp.IR[63];
                 }
             } else if (n == 128) {
-                ++kc; root = hp.push_fill(kc, pack(key, id), id, pc, root, rootI); hp.R[63] = root; hp.IR[63] = rootI;
+                ++kc; root = hp.push_fill(kc, pack(key, id), id, pc, root, rootI);
             } else {
                 ++kc; hp.push(kc, pack(key, id), id); root = hp.R[63]; rootI = hp.IR[63];
             }

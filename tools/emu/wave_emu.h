@@ -44,7 +44,9 @@ struct Heap {
     u64 L[W], R[W];
     int32_t IL[W], IR[W];
     bool holds(int32_t v) const { for (int l = 0; l < W; ++l) if (IL[l] == v || IR[l] == v) return true; return false; }
+    // Heap::replace128, straight-line (every case a lane mask; lane 63's R / IR hold the root on return)
     u64 replace128(u64 vnew, int32_t vnewI, const PathConst &pc, int32_t &rootI) {
+        constexpr u64 kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const u64 val = L[63]; const int32_t valI = IL[63];
         bool t[W];
         for (int l = 0; l < W; ++l) t[l] = L[l] > R[l];
@@ -56,34 +58,33 @@ struct Heap {
         for (int l = 0; l < W; ++l) t[l] = !(val > chv[l]);
         const u64 mv = ballot(t);
         const u64 Wm = pc.path(mv, lm);
-        u64 rootv = val; int32_t rI = valI; u32 last = 64u;
-        if (Wm) {
-            last = 63u - (u32)__builtin_clzll(Wm);
-            for (int l = 0; l < W; ++l) {
-                const bool atlast = l == (int)last;
-                const u64 up = atlast ? val : up0[l]; const int32_t upI = atlast ? valI : up0I[l];
-                if ((Wm & lm) >> l & 1) { L[l] = up; IL[l] = upI; }
-                if ((Wm & ~lm) >> l & 1) { R[l] = up; IR[l] = upI; }
-            }
-            if (Wm & 1ull) { rootv = chv[0]; rI = chI[0]; }
-        }
-        constexpr u64 kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
-        constexpr u64 kAncL = kHold & ~(1ull << 63);
-        for (int l = 0; l < W; ++l) t[l] = vnew > L[l];
-        const int h = __builtin_popcountll(ballot(t) & kAncL) + (sgt64(vnew, rootv) ? 1 : 0);
-        if (h == 0) { L[63] = vnew; IL[63] = vnewI; rootI = rI; return rootv; }
+        const int last = 63 - __builtin_clzll(Wm | 1ull);
+        const bool r0 = (Wm & 1ull) != 0ull;
+        const u64 rootv = r0 ? chv[0] : val; const int32_t rI = r0 ? chI[0] : valI;
+        const u64 wlm = Wm & lm, wrm = Wm & ~lm;
         u64 fl[W]; int32_t flI[W];
         for (int l = 0; l < W; ++l) {
-            const u32 k = (u32)l >> 1; const bool moved = ((Wm & lm) >> k) & 1ull; const bool klast = k == last;
+            const u32 half = (u32)l >> 1;
+            const bool moved = (((u32)wlm >> half) & 1u) != 0u, klast = half == (u32)last;
             fl[l] = moved ? (klast ? val : chv[l]) : fpre[l]; flI[l] = moved ? (klast ? valI : chI[l]) : fpreI[l];
+            const bool atlast = l == last;
+            const u64 up = atlast ? val : up0[l]; const int32_t upI = atlast ? valI : up0I[l];
+            if ((wlm >> l) & 1) { L[l] = up; IL[l] = upI; }
+            if ((wrm >> l) & 1) { R[l] = up; IR[l] = upI; }
         }
-        const u64 wm = kHold & (~0ull << ((1u << (7 - h)) - 1u));
-        for (int l = 0; l < W; ++l) if ((wm >> l) & 1) { L[l] = fl[l]; IL[l] = flI[l]; }
-        if (h == 7) { L[0] = rootv; IL[0] = rI; rootI = vnewI; return vnew; }
-        const int sx = (1u << (6 - h)) - 1u;
-        L[sx] = vnew; IL[sx] = vnewI;
-        rootI = rI;
-        return rootv;
+        for (int l = 0; l < W; ++l) t[l] = vnew > (l == 63 ? rootv : L[l]);
+        const int h = __builtin_popcountll(ballot(t) & kHold);
+        fl[0] = rootv; flI[0] = rI;
+        const u64 shm = h ? kHold & (~0ull << ((1u << (7 - h)) - 1u)) : 0ull;
+        const u64 xm = h < 7 ? 1ull << ((1u << (6 - h)) - 1u) : 0ull;
+        for (int l = 0; l < W; ++l) {
+            if ((shm >> l) & 1) { L[l] = fl[l]; IL[l] = flI[l]; }
+            if ((xm >> l) & 1) { L[l] = vnew; IL[l] = vnewI; }
+        }
+        const u64 nroot = h == 7 ? vnew : rootv;
+        rootI = h == 7 ? vnewI : rI;
+        R[63] = nroot; IR[63] = rootI;
+        return nroot;
     }
     u64 push_fill(int k, u64 val, int32_t valI, const PathConst &pc, u64 rootv, int32_t &rootI) {
         const u32 s1 = (u32)k; const int B = bitlen(s1);
@@ -106,6 +107,7 @@ struct Heap {
                 if (OL & 1ull) { L[0] = rootv; IL[0] = rootI; }
                 if (OR & 1ull) { R[0] = rootv; IR[0] = rootI; }
                 rootI = valI;
+                R[63] = val; IR[63] = valI;
                 return val;
             }
         }
