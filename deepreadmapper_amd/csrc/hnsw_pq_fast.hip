@@ -607,6 +607,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
     const int ef = FIX128 ? 128 : a.ef, k = (FIX128 && LOGRES) ? 128 : a.k, deg0 = a.deg0;
     const int ef_search = FIX128 ? 128 : a.efSearch;
+    const int hop_bound = a.ntotal < (int64_t)INT32_MAX ? (int)a.ntotal : INT32_MAX;
     const PathConst pconst(lane);
     const uint32_t kInfKey = ord32(INFINITY);
 
@@ -710,6 +711,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         int nstep = 0, ndis0 = 0;
         bool overrun = false;
         int32_t pred = -1;
+        // the predicted next pop_min key (the prediction's minimum): pop_min checks it with two ballots and reduces
+        // over the wave only when it missed
+        uint32_t dhint = 0xFFFFFFFFu;
         // a 2048-bit filter of the popped nodes (one bit per lane and word: 64 x 32), so the next-row prediction can
         // skip links back to nodes already expanded
         uint32_t popped_bits = 0u;
@@ -719,7 +723,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
             // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the
             // bookkeeping is broken -- end the query with an error status rather than loop
-            if (nstep > a.ntotal) {
+            if (nstep > hop_bound) {
                 overrun = true;
                 break;
             }
@@ -729,9 +733,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest
             const bool pickR = cR < cL || (cR == cL && lane != 63); // lane masks, no per-lane selects
             const uint32_t pk = pickR ? cR : cL;
-            const uint32_t d0 = wave_min_u32(pk);
+            // the minimum: the hint when no slot is below it and one holds it, else a wave reduction
+            uint32_t d0 = ufirst(dhint);
+            uint64_t eqm = ballot(pk == d0);
+            const uint64_t ltm = ballot(pk < d0);
+            if (ltm != 0ull || eqm == 0ull) {
+                d0 = wave_min_u32(pk);
+                eqm = ballot(pk == d0);
+            }
             const uint64_t rightm = ballot(pickR);
-            const uint64_t tiedm = ballot(pk == d0) & ~(rightm & (1ull << 63)); // lane 63's R is slot 0, lowest
+            const uint64_t tiedm = eqm & ~(rightm & (1ull << 63)); // lane 63's R is slot 0, lowest
             int wl = 63;
             bool wR = true;
             if (tiedm) {
@@ -740,11 +751,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             const int32_t v0 = (int32_t)((uint32_t)__builtin_amdgcn_readlane((int)lo32(wR ? hp.R : hp.L), wl) ^
                                          0x80000000u);
-            if (lane == wl) {
-                if (wR)
-                    hp.R = (hp.R & ~0xFFFFFFFFull) | kPopLo;
-                else
-                    hp.L = (hp.L & ~0xFFFFFFFFull) | kPopLo;
+            { // mark the slot popped (its id -1 in the key; IL / IR keep the node)
+                const uint64_t wm = 1ull << wl;
+                const bool mR = in_mask(wR ? wm : 0ull), mL = in_mask(wR ? 0ull : wm);
+                hp.R = mR ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
+                hp.L = mL ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
             }
             if (wl == 63 && wR)
                 root = (root & ~0xFFFFFFFFull) | kPopLo;
@@ -779,7 +790,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (!hit)
                 praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
             const int32_t v1 = lane < deg0 ? (int32_t)praw.x : -1;
-            const uint2 c8 = lane < deg0 ? make_uint2(praw.y, praw.z) : make_uint2(0u, 0u);
+            const uint2 c8 = make_uint2(praw.y, praw.z); // past deg0: link 0's code (the LUT reads stay in the LUT)
             const uint64_t negm = ballot(v1 < 0);
             const int jmax = negm ? __builtin_ctzll(negm) : 64; // lanes past deg0 hold -1
             const uint64_t actm = negm ? (negm & (0ull - negm)) - 1ull : ~0ull;
@@ -790,6 +801,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // smallest valid heap slot or link not known to be popped; its row is fetched now and waited for at
             // the next hop
             const uint32_t dall = adc8(lut, c8);
+#ifndef DRM_PQ_NOPRED // timing experiment only: no prediction, every row loaded at its hop
             {
                 const uint32_t hv = pop_hash(v1);
                 const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
@@ -799,8 +811,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
                 uint32_t mk = dp < hL ? dp : hL;
                 mk = mk < hR ? mk : hR;
-                const int32_t mid = dp == mk ? v1 : (hL == mk ? unpack_id(hp.L) : unpack_id(hp.R));
+                const int32_t hid = hL == mk ? unpack_id(hp.L) : unpack_id(hp.R);
+                const int32_t mid = dp == mk ? v1 : hid;
                 const uint32_t mm = wave_min_u32(mk);
+                dhint = mm;
                 pred = -1;
                 // no prediction (the heap and the row hold nothing valid): load v0's row again, pred stays -1
                 int32_t pnode = v0;
@@ -817,6 +831,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 #endif
                 praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
             }
+#endif
             if (STATS) {
                 // VisitedTable get + set of every link, in row order (lanes of one atomic instruction that share a
                 // word are serialised: exactly one finds a repeated id fresh); the count is all it feeds
