@@ -137,10 +137,14 @@ struct PathConst {
     // heap filling (push_fill): this lane's slots 2p+1, 2p+2 as 1-based positions 2p+2, 2p+3 share the bit
     // length bl; their father is slot p, held by lane (p-1)/2 (the L half when p is odd; the root for p = 0)
     uint32_t c2, bl, addrF;
+    // full-heap push: the chain index of this lane's L half on slot 127's ancestor chain (slot 127 = 0, 63 = 1, 31 = 2,
+    // 15 = 3, 7 = 4, 3 = 5, 1 = 6: lanes 63, 31, 15, 7, 3, 1, 0); 15 for every other lane
+    uint32_t cidx;
     __device__ explicit PathConst(int lane)
         : addrL((uint32_t)((2 * lane + 1) & 63) << 2), addrR((uint32_t)((2 * lane + 2) & 63) << 2),
           addrHalf((uint32_t)(lane >> 1) << 2), half((uint32_t)lane >> 1), c2(2u * (uint32_t)lane + 2u), bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)),
-          addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 0u)
+          addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 0u),
+          cidx(((lane + 1) & lane) == 0 ? 6u - (uint32_t)(31 - __builtin_clz((uint32_t)lane + 1u)) : 15u)
     {
         uint64_t A = 1ull << lane, Aup = 0, Lreq = 0;
         for (int c = lane; c > 0;) {
@@ -286,7 +290,8 @@ struct Heap {
     //    pre-pop value: the only cross-lane part is the pre-pop fetch.
     // Straight-line: every case is a lane mask (no branch), and lane 63's R (the root) is current on return. Returns
     // the root after the push, its id in rootI.
-    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int32_t &rootI)
+    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int lane,
+                                                   int32_t &rootI)
     {
         constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const uint64_t val = readlane64(L, 63); // slot 127
@@ -302,23 +307,23 @@ struct Heap {
         const int32_t fpreI = bperm32_addr(IL, pc.addrHalf);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
-        const int last = 63 - __builtin_clzll(W | 1ull); // the path's deepest node (read only under W)
+        // per-lane tests, no scalar bit arithmetic: the path is a chain of nodes, so its deepest node p is the one
+        // with W >> p == 1
+        const bool atlast = (W >> lane) == 1ull;
+        const bool klast = (W >> pc.half) == 1ull;
+        const bool moved = ((W & lm) >> pc.half) & 1ull; // lane (lane >> 1) is on the path and took its L child
         const uint64_t c0 = readlane64(chv, 0);
         const int32_t c0I = readlane32(chI, 0);
         const bool r0 = (W & 1ull) != 0ull; // the root's larger child moves up
         const uint64_t rootv = r0 ? c0 : val;
         const int32_t rI = r0 ? c0I : valI;
-        // pop writes: the path nodes' chosen child slots
-        const bool atlast = in_mask(1ull << last);
-        const uint64_t up = atlast ? val : up0;
-        const int32_t upI = atlast ? valI : up0I;
-        const uint64_t wlm = W & lm;
-        // the chain's fathers after the pop (lane 0's is the root)
-        const bool moved = (((uint32_t)wlm >> pc.half) & 1u) != 0u;
-        const bool klast = pc.half == (uint32_t)last;
+        // the chain's fathers after the pop (lane 0's is the root), from the pre-pop registers
         uint64_t fl = moved ? (klast ? val : chv) : fpre;
         int32_t flI = moved ? (klast ? valI : chI) : fpreI;
-        const bool wl = in_mask(wlm), wr = in_mask(W & ~lm);
+        // pop writes: the path nodes' chosen child slots
+        const uint64_t up = atlast ? val : up0;
+        const int32_t upI = atlast ? valI : up0I;
+        const bool wl = in_mask(W & lm), wr = in_mask(W & ~lm);
         L = wl ? up : L;
         IL = wl ? upI : IL;
         R = wr ? up : R;
@@ -330,14 +335,11 @@ struct Heap {
         const bool s1 = in_mask(1ull);
         fl = s1 ? rootv : fl;
         flI = s1 ? rI : flI;
-        // chain index m (slot 127 = 0, 63 = 1, ..., 1 = 6; the root = 7) is lane (1 << (6 - m)) - 1's L half: the
-        // indices below h take their father's value, index h takes vnew
-        const uint64_t shm = h ? kHold & (~0ull << ((1u << (7 - h)) - 1u)) : 0ull;
-        const bool sh = in_mask(shm);
+        // the chain indices below h take their father's value, index h takes vnew (h = 7: the root)
+        const bool sh = pc.cidx < (uint32_t)h;
         L = sh ? fl : L;
         IL = sh ? flI : IL;
-        const uint64_t xm = h < 7 ? 1ull << ((1u << (6 - h)) - 1u) : 0ull;
-        const bool xs = in_mask(xm);
+        const bool xs = pc.cidx == (uint32_t)h;
         L = xs ? vnew : L;
         IL = xs ? vnewI : IL;
         const uint64_t nroot = h == 7 ? vnew : rootv;
@@ -655,7 +657,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         hp.R = lane == 63 ? pack(dn, nearest) : kUnused;
         hp.IL = -1;
         hp.IR = lane == 63 ? nearest : -1;
-        int kc = 1, nvalid = 1;
+        int kc = 1;
         uint64_t root = pack(dn, nearest); // slot 0
         int32_t rootI = nearest;
         // result set: the log (LOGRES) or a sorted register set of k <= 64 entries
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         uint32_t popped_bits = 0u;
         Link3 praw{0xFFFFFFFFu, 0u, 0u}; // the predicted row's link `lane`, raw (pred = -1: none yet)
         auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
-        while (nvalid > 0) {
+        for (;;) {
             // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
             // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the
             // bookkeeping is broken -- end the query with an error status rather than loop
@@ -729,6 +731,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             // pop_min: smallest key among valid slots, ties -> the highest slot
             const bool vL = lo32(hp.L) != kPopLo, vR = lo32(hp.R) != kPopLo;
+            // MinimaxHeap::size(): the valid (filled, not popped) slots; unused slots read as popped
+            const uint64_t validm = ballot(vL) | ballot(vR);
+            if (validm == 0ull)
+                break;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
             // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest
             const bool pickR = cR < cL || (cR == cL && lane != 63); // lane masks, no per-lane selects
@@ -759,8 +765,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             if (wl == 63 && wR)
                 root = (root & ~0xFFFFFFFFull) | kPopLo;
-            nvalid--;
-            DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)nvalid, (uint32_t)kc, hi32(root));
+            DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)__builtin_popcountll(validm), (uint32_t)kc, hi32(root));
             // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
             const int below = __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
             if (below >= ef_search)
@@ -782,7 +787,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 #ifdef DRM_PQ_DEBUG
             if (v0 < 0 || v0 >= a.ntotal) {
                 if (lane == 0)
-                    printf("[pq dbg] q %d hop %d: v0 %d out of range (nvalid %d kc %d d0 %08x)\n", q, nstep, v0, nvalid, kc, d0);
+                    printf("[pq dbg] q %d hop %d: v0 %d out of range (kc %d d0 %08x)\n", q, nstep, v0, kc, d0);
                 overrun = true;
                 break;
             }
@@ -867,7 +872,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (hp.holds(idl))
                         continue;
                     const uint64_t val = pack(key, idl);
-                    DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
+                    DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, 0u, (uint32_t)sn);
                     if (!LOGRES && key < thr)
                         add_result(val);
                     ++kc;
@@ -878,7 +883,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         root = readlane64(hp.R, 63);
                         rootI = readlane32(hp.IR, 63);
                     }
-                    ++nvalid;
                 }
                 if (kc == ef)
                     rem &= ballot(dall < hi32(root));
@@ -887,7 +891,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             }
             while (rem) { // MinimaxHeap::push on the full heap: pop the max, push val
                 const int l = __builtin_ctzll(rem);
-                rem &= rem - 1;
+                asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
                 const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
                 if (key >= hi32(root))
                     continue;
@@ -897,14 +901,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 if (hp.holds(idl))
                     continue;
                 const uint64_t val = pack(key, idl);
-                DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, (uint32_t)nvalid, (uint32_t)sn);
+                DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, 0u, (uint32_t)sn);
                 if (!LOGRES && key < thr)
                     add_result(val);
                 const uint32_t evk = hi32(root); // the evicted slot: the root (its node id in rootI)
                 const int32_t evi = rootI;
-                nvalid += lo32(root) == kPopLo ? 1 : 0; // --nvalid unless the evicted slot was popped; ++nvalid
                 if (ef == 128) {
-                    root = hp.replace128(val, idl, pconst, rootI);
+                    root = hp.replace128(val, idl, pconst, lane, rootI);
                     if (STAMPS)
                         st_acc[11] += 1u;
                 } else {
