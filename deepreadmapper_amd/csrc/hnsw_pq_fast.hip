@@ -736,8 +736,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (validm == 0ull)
                 break;
             const uint32_t cL = vL ? hi32(hp.L) : 0xFFFFFFFFu, cR = vR ? hi32(hp.R) : 0xFFFFFFFFu;
-            // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest
-            const bool pickR = cR < cL || (cR == cL && lane != 63); // lane masks, no per-lane selects
+            // in-lane: slot 2l+2 (R) outranks 2l+1 (L); lane 63's R is slot 0, the lowest (a mask, not a lane value)
+            const uint64_t rightm = ballot(cR < cL) | (ballot(cR == cL) & ~(1ull << 63));
+            const bool pickR = in_mask(rightm);
             const uint32_t pk = pickR ? cR : cL;
             // the minimum: the hint when no slot is below it and one holds it, else a wave reduction
             uint32_t d0 = ufirst(dhint);
@@ -747,23 +748,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 d0 = wave_min_u32(pk);
                 eqm = ballot(pk == d0);
             }
-            const uint64_t rightm = ballot(pickR);
-            const uint64_t tiedm = eqm & ~(rightm & (1ull << 63)); // lane 63's R is slot 0, lowest
-            int wl = 63;
-            bool wR = true;
-            if (tiedm) {
-                wl = 63 - __builtin_clzll(tiedm);
-                wR = (rightm >> wl) & 1ull;
-            }
-            const int32_t v0 = (int32_t)((uint32_t)__builtin_amdgcn_readlane((int)lo32(wR ? hp.R : hp.L), wl) ^
+            // the highest tied slot: the highest tied lane, unless that is lane 63 holding the root (slot 0)
+            const uint64_t tiedm = eqm & ~(rightm & (1ull << 63));
+            const int wl = tiedm ? 63 - __builtin_clzll(tiedm) : 63;
+            const int32_t v0 = (int32_t)((uint32_t)__builtin_amdgcn_readlane((int)lo32(pickR ? hp.R : hp.L), wl) ^
                                          0x80000000u);
             { // mark the slot popped (its id -1 in the key; IL / IR keep the node)
-                const uint64_t wm = 1ull << wl;
-                const bool mR = in_mask(wR ? wm : 0ull), mL = in_mask(wR ? 0ull : wm);
-                hp.R = mR ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
-                hp.L = mL ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
+                const bool win = lane == wl;
+                hp.R = (win && pickR) ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
+                hp.L = (win && !pickR) ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
             }
-            if (wl == 63 && wR)
+            if (wl == 63 && (rightm >> 63))
                 root = (root & ~0xFFFFFFFFull) | kPopLo;
             DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)__builtin_popcountll(validm), (uint32_t)kc, hi32(root));
             // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
