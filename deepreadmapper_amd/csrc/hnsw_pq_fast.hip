@@ -10,10 +10,12 @@
 //   * the heap sits in the sibling-pair layout (lane p holds the children of node p, slots 2p+1 and
 //     2p+2; the root is lane 63's second half); a full-heap replace finds its sift-down path from two
 //     ballots and per-lane ancestor masks, and its sift-up chain by one parallel compare;
-//   * pop_min is one 32-bit DPP min plus a ballot for the highest tied slot;
+//   * pop_min checks the previous hop's prediction of the minimum with two ballots (a 32-bit DPP min
+//     only when it missed) and takes the highest tied slot from lane masks;
 //   * result set at k == ef: the HeapBlockResultHandler (k = ef) holds, at every step, the same
-//     multiset of distances as the MinimaxHeap, so the kernel logs every accepted push and selects +
-//     sorts the k results once per query. k < ef keeps a register result set (k <= 64);
+//     multiset of distances as the MinimaxHeap, and the heap slots carry node ids, so the k results are
+//     the heap's entries plus the evicted ones that tied with the root they left (a log of those alone);
+//     selected + sorted once per query. k < ef keeps a register result set (k <= 64);
 //   * no visited table. faiss's VisitedTable answers "was this link seen before?"; the kernel answers it
 //     from the heap instead ("The heap is the visited set"). Every heap slot also
 //     carries its node id (IL / IR), popped or not. A link whose distance is at or above the root of the
@@ -801,7 +803,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // smallest valid heap slot or link not known to be popped; its row is fetched now and waited for at
             // the next hop
             const uint32_t dall = adc8(lut, c8);
-#ifndef DRM_PQ_NOPRED // timing experiment only: no prediction, every row loaded at its hop
             {
                 const uint32_t hv = pop_hash(v1);
                 const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
@@ -831,7 +832,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
 #endif
                 praw = load_link_raw(a.rows + (size_t)pnode * (size_t)a.row_words, lane, deg0);
             }
-#endif
             if (STATS) {
                 // VisitedTable get + set of every link, in row order (lanes of one atomic instruction that share a
                 // word are serialised: exactly one finds a repeated id fresh); the count is all it feeds
