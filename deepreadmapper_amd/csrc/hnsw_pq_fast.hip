@@ -879,11 +879,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         rootI = readlane32(hp.IR, 63);
                     }
                 }
-                if (kc == ef)
-                    rem &= ballot(dall < hi32(root));
-            } else {
-                rem &= ballot(dall < hi32(root));
             }
+            rem &= ballot(dall < hi32(root)); // the heap is full here, or rem is empty
             while (rem) { // MinimaxHeap::push on the full heap: pop the max, push val
                 const int l = __builtin_ctzll(rem);
                 asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
