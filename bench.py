@@ -169,8 +169,10 @@ def cpu_baseline(refs, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat
     ts, tw = run(n)
     log_fn(f"[cpu] oracle on {n} queries x {threads} threads: search {ts:.2f}s, SW {tw:.2f}s")
     return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of this rank's reads (oracle/ C restatement, OpenMP {threads} threads on "
-                      f"{cpu_model()}): search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+            "node_cpus": os.cpu_count(),
+            "sample": f"first {n} of this rank's reads (oracle/ C restatement, OpenMP {threads} threads -- the "
+                      f"process's CPU lease -- of the node's {os.cpu_count()} logical CPUs, {cpu_model()}): "
+                      f"search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
 
 
 def prepare_c3(args, D, dev):
