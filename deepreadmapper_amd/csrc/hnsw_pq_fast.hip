@@ -885,8 +885,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const int l = __builtin_ctzll(rem);
                 asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
                 const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
-                if (key >= hi32(root))
-                    continue;
                 const int32_t idl = __builtin_amdgcn_readlane(v1, l);
                 if (STAMPS)
                     st_acc[4] += 1u;
@@ -908,6 +906,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     root = readlane64(hp.R, 63);
                     rootI = readlane32(hp.IR, 63);
                 }
+                // the root fell: links at or above it leave the candidate mask (one compare for the rest of the row)
+                rem &= ballot(dall < hi32(root));
                 // LOGRES: an evicted result at the new root's distance can still be among the k results (the result
                 // handler breaks distance ties by node id, the MinimaxHeap by slot); any other evicted one cannot
                 if (LOGRES && evk == hi32(root)) {

@@ -91,12 +91,13 @@ extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t
         while (rem) { // the full heap: pop the max, push val; log an evicted entry tied with the new root
             const int l = __builtin_ctzll(rem); rem &= rem - 1;
             const u32 key = dall[l];
-            if (key >= hi32(root)) continue;
+            if (key >= hi32(root)) { std::printf("candidate at or above the root at hop %d\n", nstep); return -5; }
             const int32_t idl = v1[l];
             if (hp.holds(idl)) continue;
             const u32 evk = hi32(root); const int32_t evi = rootI;
             nvalid += lo32(root) == kPopLo ? 1 : 0;
             root = hp.replace128(pack(key, idl), idl, pc, rootI);
+            rem &= below_root(); // the root fell: links at or above it leave the mask
             if (evk == hi32(root)) lg.push_back(pack(evk, evi));
             pushed.push_back(idl);
         }
