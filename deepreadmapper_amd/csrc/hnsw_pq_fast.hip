@@ -124,7 +124,9 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 #pragma unroll
     for (int m = 0; m < 8; ++m)
         r = __fadd_rn(r, lv[m]);
-    return ord32(r);
+    // ord32 of a sum of non-negative LUT entries (squared sub-distances, summed from +0.0): the sign bit is clear,
+    // so ord32(r) is r's bit pattern with the sign bit set -- one op instead of ord32's select
+    return __float_as_uint(r) | 0x80000000u;
 }
 
 // Per-lane constants of node p = lane: A = p and its ancestors, Aup = its ancestors, Lreq = the
