@@ -367,7 +367,7 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 #define DRM_SW_ROWS 2 // DP rows in flight per pass over the columns (sw_rows_i16); 2 measured fastest of 2-5
 #endif
 #ifndef DRM_SW_PF
-#define DRM_SW_PF 2 // profile groups (4 columns each) read ahead of the one in use, per row
+#define DRM_SW_PF 1 // profile groups (4 columns each) read ahead of the one in use, per row (1-4 measured: 1 best by <1 %)
 #endif
 
 // ---- integer cells. A score s (0 <= s <= 1023) is the 16-bit pattern s, i.e. the fp16 subnormal s * 2^-24: fp16
