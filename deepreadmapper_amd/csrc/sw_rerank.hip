@@ -654,38 +654,50 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
 
 // Kernel 2 of the rerank: sw_reranker's std::partial_sort + output, one thread per query. Each
 // thread replays libstdc++'s heap algorithm on its own padded LDS array (stride cmax+1 words, so
-// threads touching the same heap index hit different banks).
+// threads touching the same heap index hit different banks). The block loads its queries' score rows and writes
+// their results cooperatively (one query row at a time, lanes along the row: coalesced), around the per-thread sort.
 __global__ __launch_bounds__(64) void sw_topk_kernel(RerankArgs a)
 {
     extern __shared__ uint32_t heap_lds[];
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= a.nq)
-        return;
-    uint32_t *e = heap_lds + (size_t)threadIdx.x * (size_t)(a.cmax + 1);
-    const int ncand = a.ncand[q];
-    int status;
-    if (ncand < 0)
-        status = ncand; // -2: > kMaxCands candidates, -3: query longer than the SW build
-    else if (ncand == 0 || a.k == 0)
-        status = 0; // reranker.cpp:10-11: empty result for this query
-    else if (ncand < a.k)
-        status = -1; // reranker.cpp:26-29
-    else
-        status = a.k;
-    a.status[q] = status;
-    if (status > 0) {
-        for (int c = 0; c < ncand; ++c)
-            e[c] = ((uint32_t)a.cand_scores[q * a.cmax + c] << 16) | (uint32_t)c;
-        ps_partial_sort(e, ncand, a.k);
-        for (int j = 0; j < a.k; ++j) {
-            const uint32_t v = e[j];
-            a.top_scores[q * a.k + j] = (int32_t)(v >> 16);
-            a.top_ids[q * a.k + j] = a.cand_ids[q * a.cmax + (v & 0xFFFFu)];
-        }
-    } else {
-        for (int j = 0; j < a.k; ++j) {
-            a.top_scores[q * a.k + j] = -1;
-            a.top_ids[q * a.k + j] = ~0ull;
+    __shared__ int ncand_s[64], status_s[64];
+    const int tpb = (int)blockDim.x, t = (int)threadIdx.x;
+    const int64_t q0 = (int64_t)blockIdx.x * tpb;
+    const int nqb = (int)((a.nq - q0) < tpb ? (a.nq - q0) : tpb);
+    const int stride = a.cmax + 1;
+    if (t < nqb) {
+        const int ncand = a.ncand[q0 + t];
+        int status;
+        if (ncand < 0)
+            status = ncand; // -2: > kMaxCands candidates, -3: query longer than the SW build
+        else if (ncand == 0 || a.k == 0)
+            status = 0; // reranker.cpp:10-11: empty result for this query
+        else if (ncand < a.k)
+            status = -1; // reranker.cpp:26-29
+        else
+            status = a.k;
+        ncand_s[t] = ncand;
+        status_s[t] = status;
+        a.status[q0 + t] = status;
+    }
+    __syncthreads();
+    for (int r = 0; r < nqb; ++r) { // the rows' (score, candidate) words, packed as the sort compares them
+        if (status_s[r] <= 0)
+            continue;
+        const int nc = ncand_s[r];
+        for (int c = t; c < nc; c += tpb)
+            heap_lds[(size_t)r * stride + c] = ((uint32_t)a.cand_scores[(q0 + r) * a.cmax + c] << 16) | (uint32_t)c;
+    }
+    __syncthreads();
+    if (t < nqb && status_s[t] > 0)
+        ps_partial_sort(heap_lds + (size_t)t * stride, ncand_s[t], a.k);
+    __syncthreads();
+    for (int r = 0; r < nqb; ++r) {
+        const int64_t q = q0 + r;
+        const bool ok = status_s[r] > 0;
+        for (int j = t; j < a.k; j += tpb) {
+            const uint32_t v = ok ? heap_lds[(size_t)r * stride + j] : 0u;
+            a.top_scores[q * a.k + j] = ok ? (int32_t)(v >> 16) : -1;
+            a.top_ids[q * a.k + j] = ok ? a.cand_ids[q * a.cmax + (v & 0xFFFFu)] : ~0ull;
         }
     }
 }
