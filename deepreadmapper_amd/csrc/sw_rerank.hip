@@ -794,6 +794,13 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         gcap = (int64_t)std::max(cus, 1) * refs.sw_waves_per_cu;
     }
     const int grid = (int)std::min<int64_t>(a.nq, gcap);
+#ifndef DRM_SW_F16_GRID_CAP
+#define DRM_SW_F16_GRID_CAP (1 << 30)
+#endif
+    // the pair-profile kernel: one workgroup per query (a query is ~270k issue cycles of one wave, so the grid's
+    // tail is one query, not the 19-20 a 65536-wave grid-stride hands each wave at C5)
+    const int grid_f16 =
+        (int)std::min<int64_t>(a.nq, refs.sw_waves_per_cu > 0 ? gcap : (int64_t)DRM_SW_F16_GRID_CAP);
     const size_t cand_lds = sizeof(uint32_t) * (size_t)cmax; // sw_score_f16_kernel's candidate list
     // fp16 pair-profile kernel for queries up to 152 bytes; the bit-profile kernel re-scores the
     // queries it flagged, and takes longer queries (or everything when DRM_SW_BITPROFILE=1).
@@ -806,7 +813,7 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         if (force_bits) {
             hipLaunchKernelGGL((sw_score_kernel<64>), dim3(grid), dim3(64), 0, stream, a);
         } else {
-            hipLaunchKernelGGL((sw_score_f16_kernel<64>), dim3(grid), dim3(64), cand_lds, stream, a);
+            hipLaunchKernelGGL((sw_score_f16_kernel<64>), dim3(grid_f16), dim3(64), cand_lds, stream, a);
             hipLaunchKernelGGL((sw_score_kernel<64, true>), dim3(grid), dim3(64), 0, stream, a);
         }
         break;
@@ -816,7 +823,7 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         } else {
             // 150 DP columns: the read's bases; the "<" / ">" tags are dropped in the kernel (a query with more
             // than 150 columns left after its non-ACGT ends is flagged and scored by the bit-profile kernel)
-            hipLaunchKernelGGL((sw_score_f16_kernel<150>), dim3(grid), dim3(64), cand_lds, stream, a);
+            hipLaunchKernelGGL((sw_score_f16_kernel<150>), dim3(grid_f16), dim3(64), cand_lds, stream, a);
             hipLaunchKernelGGL((sw_score_kernel<152, true>), dim3(grid), dim3(64), 0, stream, a);
         }
         break;
