@@ -39,6 +39,10 @@ SW_VALU_PER_CELL_PAIR = 1053 / 300  # static ISA count of sw_score_f16_kernel<15
 # its mix (integer cells, DRM_SW_INT): 751 packed 16-bit (v_pk_maximum3_f16, v_pk_sub_u16) at 4 cycles per wave64
 # instruction per SIMD and 302 32-bit (v_add_u32, ...) at 2 (profiles/r02/valu_rate_probe.txt): average issue cycles
 SW_ISSUE_CYC_PER_VALU = (751 * 4.0 + 302 * 2.0) / 1053
+# what that exact mix (per cell pair: v_add_u32, v_pk_maximum3_f16, v_pk_sub_u16 clamp, half a v_pk_maximum3_f16),
+# free of memory and dependency stalls, issues at on one MI355X: cycles per cell pair per SIMD at the nominal clock,
+# at the kernel's 2 waves per SIMD and at 8 (tools/microbench/valu_rate.hip, profiles/r04/valu_rate_mix.txt)
+SW_MIX_CYC_PER_PAIR = {2: 4.31 * 3.5, 8: 3.98 * 3.5}
 
 
 def cpu_model():
@@ -745,6 +749,8 @@ def main():
     if sw_pmc and "SQ_INSTS_VALU" in sw_pmc and (Q, K) == (1_250_000, 128):
         sw_instr, sw_instr_src = float(sw_pmc["SQ_INSTS_VALU"]), f"{sw_prof_path}: SQ_INSTS_VALU per dispatch"
     sw_achieved_cyc = sw_instr * SW_ISSUE_CYC_PER_VALU / (sw_ms * 1e-3)
+    # the whole rerank's time (scoring, top-k, flagged re-scores) per DP cell pair per SIMD, against the mix floor
+    sw_cyc_pair = (sw_ms * 1e-3) * CLOCK_HZ * ncu * 4 / (dp_cells / 2.0 / 64.0)
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
@@ -798,7 +804,14 @@ def main():
                             "issue_cycles_per_cell_pair": round(SW_VALU_PER_CELL_PAIR * SW_ISSUE_CYC_PER_VALU, 2),
                             "note": "frac = VALU issue cycles used (packed 16-bit 4, 32-bit 2 cycles per wave64 "
                                     "instruction) / the SIMDs' capacity (1,024 SIMDs x 2.4 GHz); the DP's op count per "
-                                    "cell pair is reported separately"},
+                                    "cell pair is reported separately",
+                            "mix_floor": {"rerank_cycles_per_cell_pair": round(sw_cyc_pair, 2),
+                                          "floor_cycles_per_cell_pair_2_waves": round(SW_MIX_CYC_PER_PAIR[2], 2),
+                                          "floor_cycles_per_cell_pair_8_waves": round(SW_MIX_CYC_PER_PAIR[8], 2),
+                                          "frac_2_waves": round(SW_MIX_CYC_PER_PAIR[2] / sw_cyc_pair, 4),
+                                          "frac_8_waves": round(SW_MIX_CYC_PER_PAIR[8] / sw_cyc_pair, 4),
+                                          "source": "profiles/r04/valu_rate_mix.txt (the DP's instruction mix alone, "
+                                                    "all operands in registers; the kernel holds 2 waves per SIMD)"}},
             "cpu_baseline": cpu,
             "gather": gather,
             "gather_ok": gather_ok,
