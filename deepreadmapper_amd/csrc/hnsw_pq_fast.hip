@@ -757,18 +757,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const int wl = tiedm ? 63 - __builtin_clzll(tiedm) : 63;
             const int32_t v0 = (int32_t)((uint32_t)__builtin_amdgcn_readlane((int)lo32(pickR ? hp.R : hp.L), wl) ^
                                          0x80000000u);
-            { // mark the slot popped (its id -1 in the key; IL / IR keep the node)
-                const bool win = lane == wl;
-                hp.R = (win && pickR) ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
-                hp.L = (win && !pickR) ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
-            }
+            // mark the slot popped (its id -1 in the key; IL / IR keep the node)
+            const bool popR = lane == wl && pickR, popL = lane == wl && !pickR;
+            hp.R = popR ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
+            hp.L = popL ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
             if (wl == 63 && (rightm >> 63))
                 root = (root & ~0xFFFFFFFFull) | kPopLo;
             DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)__builtin_popcountll(validm), (uint32_t)kc, hi32(root));
-            // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0
-            const int below = __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
-            if (below >= ef_search)
-                break;
+            // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0. The slot just popped
+            // holds d0 itself, so at most ef - 1 slots lie below it: with efSearch >= ef (ef = max(efSearch, k), so
+            // whenever k <= efSearch -- the pipeline's EF = K = 128) the check can never stop the search, and is skipped
+            if (ef_search < ef) {
+                const int below =
+                    __builtin_popcountll(ballot(hi32(hp.L) < d0)) + __builtin_popcountll(ballot(hi32(hp.R) < d0));
+                if (below >= ef_search)
+                    break;
+            }
             DRM_FSTAMP(2);
 
             // expand v0's level-0 row: its ids and codes arrive with one load, prefetched one hop ago when the
@@ -810,8 +814,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const uint32_t pw = bperm32(popped_bits, (int)((hv >> 5) & 63u));
                 const bool known_popped = (pw >> (hv & 31u)) & 1u;
                 const uint32_t dp = (lane < jmax && !known_popped) ? dall : 0xFFFFFFFFu;
-                const uint32_t hL = lo32(hp.L) != kPopLo ? hi32(hp.L) : 0xFFFFFFFFu;
-                const uint32_t hR = lo32(hp.R) != kPopLo ? hi32(hp.R) : 0xFFFFFFFFu;
+                // the valid slots' keys: pop_min's, less the slot it just popped
+                const uint32_t hL = popL ? 0xFFFFFFFFu : cL;
+                const uint32_t hR = popR ? 0xFFFFFFFFu : cR;
                 uint32_t mk = dp < hL ? dp : hL;
                 mk = mk < hR ? mk : hR;
                 const int32_t hid = hL == mk ? unpack_id(hp.L) : unpack_id(hp.R);
