@@ -309,6 +309,9 @@ struct Heap {
         const int32_t up0I = bperm32_addr(chI, caddr);
         const uint64_t fpre = bperm64_addr(L, pc.addrHalf);
         const int32_t fpreI = bperm32_addr(IL, pc.addrHalf);
+        // keep the six fetches together: left to itself the compiler issues the father fetch after the first wait,
+        // which makes two LDS round trips of the one (profiles/r04/ab_search_replace_fetch_pin.txt)
+        __builtin_amdgcn_sched_barrier(0);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
         // per-lane tests, no scalar bit arithmetic: the path is a chain of nodes, so its deepest node p is the one
