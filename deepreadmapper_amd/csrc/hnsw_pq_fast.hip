@@ -727,7 +727,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // skip links back to nodes already expanded
         uint32_t popped_bits = 0u;
         Link3 praw{0xFFFFFFFFu, 0u, 0u}; // the predicted row's link `lane`, raw (pred = -1: none yet)
-        auto pop_hash = [](int32_t v) { return ((uint32_t)v * 2654435761u) >> 21; }; // 11 bits
+        // 11 bits of a 24-bit multiplicative hash (v_mul_u32_u24, full rate; a 32-bit v_mul_lo_u32 is not)
+        auto pop_hash = [](int32_t v) { return (((uint32_t)v & 0xFFFFFFu) * 0x9E3779u) >> 21; };
         for (;;) {
             // every hop expands a node taken off the heap, and a node enters the heap at most once (a node in the
             // heap is seen, one that left it is at or above the root for good): more than ntotal hops means the

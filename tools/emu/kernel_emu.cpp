@@ -9,7 +9,7 @@
 
 // ---- the lean kernel's level-0 loop (hnsw_pq_fast_kernel, LOGRES, ef = efSearch = k = 128), one query, lane by lane
 static u32 ord32(float f) { u32 u; std::memcpy(&u, &f, 4); return (u & 0x80000000u) ? ~u : (u | 0x80000000u); }
-static u32 pop_hash(int32_t v) { return ((u32)v * 2654435761u) >> 21; }
+static u32 pop_hash(int32_t v) { return (((u32)v & 0xFFFFFFu) * 0x9E3779u) >> 21; }
 
 extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t ntotal, int deg0, const float *lut,
                               int32_t nearest, float dnear, int32_t *out_ids, uint32_t *out_keys, int32_t *stats)
