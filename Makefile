@@ -29,6 +29,11 @@ $(BUILD):
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# the search kernel under the max-ILP machine scheduler: 104.3 -> 103.7 ms at C5, ids identical; the SW rerank is
+# 1-2 % slower under it, so only this file (profiles/r04/ab_search_sched_strategy.txt)
+$(BUILD)/hnsw_pq_fast.o: $(SRC)/hnsw_pq_fast.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=max-ilp -c $< -o $@
+
 $(BUILD)/capi.o: $(SRC)/capi.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
