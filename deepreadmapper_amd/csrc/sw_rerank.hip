@@ -208,16 +208,19 @@ __device__ void build_profile(uint32_t *prof, const uint8_t *q, int qlen)
 
 // ------------------------------------------------------------------------ partial_sort replay
 // libstdc++ std::partial_sort(first, middle, last, comp) with comp(a,b) = score[a] > score[b]
-// (reranker.cpp:38-40) on packed elements e = (score << 16) | index: comp only looks at score.
-__device__ __forceinline__ bool ps_comp(uint32_t a, uint32_t b) { return (a >> 16) > (b >> 16); }
+// (reranker.cpp:38-40) on packed elements e = (score << S) | index: comp only looks at score. T = uint32_t, S = 16 in
+// general; T = uint16_t, S = 8 when every score and candidate index fits a byte (half the LDS per query).
+template <typename T, int S>
+__device__ __forceinline__ bool ps_comp(T a, T b) { return (a >> S) > (b >> S); }
 
-__device__ void ps_adjust_heap(uint32_t *first, int hole, int len, uint32_t value)
+template <typename T, int S>
+__device__ void ps_adjust_heap(T *first, int hole, int len, T value)
 {
     const int top = hole;
     int second = hole;
     while (second < (len - 1) / 2) {
         second = 2 * (second + 1);
-        if (ps_comp(first[second], first[second - 1]))
+        if (ps_comp<T, S>(first[second], first[second - 1]))
             second--;
         first[hole] = first[second];
         hole = second;
@@ -228,7 +231,7 @@ __device__ void ps_adjust_heap(uint32_t *first, int hole, int len, uint32_t valu
         hole = second - 1;
     }
     int parent = (hole - 1) / 2;
-    while (hole > top && ps_comp(first[parent], value)) {
+    while (hole > top && ps_comp<T, S>(first[parent], value)) {
         first[hole] = first[parent];
         hole = parent;
         parent = (hole - 1) / 2;
@@ -236,27 +239,28 @@ __device__ void ps_adjust_heap(uint32_t *first, int hole, int len, uint32_t valu
     first[hole] = value;
 }
 
-__device__ void ps_partial_sort(uint32_t *e, int n, int k)
+template <typename T, int S>
+__device__ void ps_partial_sort(T *e, int n, int k)
 {
     if (k >= 2) { // __make_heap(first, middle)
         int parent = (k - 2) / 2;
         for (;;) {
-            ps_adjust_heap(e, parent, k, e[parent]);
+            ps_adjust_heap<T, S>(e, parent, k, e[parent]);
             if (parent == 0)
                 break;
             parent--;
         }
     }
     for (int i = k; i < n; ++i) // rest of __heap_select
-        if (ps_comp(e[i], e[0])) {
-            const uint32_t v = e[i];
+        if (ps_comp<T, S>(e[i], e[0])) {
+            const T v = e[i];
             e[i] = e[0];
-            ps_adjust_heap(e, 0, k, v);
+            ps_adjust_heap<T, S>(e, 0, k, v);
         }
     for (int last = k - 1; last > 0; --last) { // __sort_heap
-        const uint32_t v = e[last];
+        const T v = e[last];
         e[last] = e[0];
-        ps_adjust_heap(e, 0, last, v);
+        ps_adjust_heap<T, S>(e, 0, last, v);
     }
 }
 
@@ -653,17 +657,19 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
 }
 
 // Kernel 2 of the rerank: sw_reranker's std::partial_sort + output, one thread per query. Each
-// thread replays libstdc++'s heap algorithm on its own padded LDS array (stride cmax+1 words, so
+// thread replays libstdc++'s heap algorithm on its own padded LDS array (stride: an odd number of words, so
 // threads touching the same heap index hit different banks). The block loads its queries' score rows and writes
 // their results cooperatively (one query row at a time, lanes along the row: coalesced), around the per-thread sort.
-__global__ __launch_bounds__(64) void sw_topk_kernel(RerankArgs a)
+// T / S: the packed element (see ps_comp); stride in elements.
+template <typename T, int S>
+__global__ __launch_bounds__(64) void sw_topk_kernel(RerankArgs a, int stride)
 {
-    extern __shared__ uint32_t heap_lds[];
+    extern __shared__ __align__(16) unsigned char topk_lds[];
+    T *heap_lds = reinterpret_cast<T *>(topk_lds);
     __shared__ int ncand_s[64], status_s[64];
     const int tpb = (int)blockDim.x, t = (int)threadIdx.x;
     const int64_t q0 = (int64_t)blockIdx.x * tpb;
     const int nqb = (int)((a.nq - q0) < tpb ? (a.nq - q0) : tpb);
-    const int stride = a.cmax + 1;
     if (t < nqb) {
         const int ncand = a.ncand[q0 + t];
         int status;
@@ -685,19 +691,19 @@ __global__ __launch_bounds__(64) void sw_topk_kernel(RerankArgs a)
             continue;
         const int nc = ncand_s[r];
         for (int c = t; c < nc; c += tpb)
-            heap_lds[(size_t)r * stride + c] = ((uint32_t)a.cand_scores[(q0 + r) * a.cmax + c] << 16) | (uint32_t)c;
+            heap_lds[(size_t)r * stride + c] = (T)(((uint32_t)a.cand_scores[(q0 + r) * a.cmax + c] << S) | (uint32_t)c);
     }
     __syncthreads();
     if (t < nqb && status_s[t] > 0)
-        ps_partial_sort(heap_lds + (size_t)t * stride, ncand_s[t], a.k);
+        ps_partial_sort<T, S>(heap_lds + (size_t)t * stride, ncand_s[t], a.k);
     __syncthreads();
     for (int r = 0; r < nqb; ++r) {
         const int64_t q = q0 + r;
         const bool ok = status_s[r] > 0;
         for (int j = t; j < a.k; j += tpb) {
-            const uint32_t v = ok ? heap_lds[(size_t)r * stride + j] : 0u;
-            a.top_scores[q * a.k + j] = ok ? (int32_t)(v >> 16) : -1;
-            a.top_ids[q * a.k + j] = ok ? a.cand_ids[q * a.cmax + (v & 0xFFFFu)] : ~0ull;
+            const uint32_t v = ok ? (uint32_t)heap_lds[(size_t)r * stride + j] : 0u;
+            a.top_scores[q * a.k + j] = ok ? (int32_t)(v >> S) : -1;
+            a.top_ids[q * a.k + j] = ok ? a.cand_ids[q * a.cmax + (v & ((1u << S) - 1u))] : ~0ull;
         }
     }
 }
@@ -832,12 +838,22 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
         break;
     }
     DRM_HIP_CHECK(hipGetLastError());
+    // 16-bit elements when every score (<= the window length) and every candidate index fits a byte: half the LDS
+    // per query, twice the queries in flight for the latency-bound heap walk
+    const bool small = a.ref_len <= 255 && cmax <= 256;
+    const size_t esz = small ? 2 : 4;
+    const int stride_words = (int)(((size_t)(cmax + 1) * esz + 3) / 4) | 1; // odd: lanes at one index, distinct banks
+    const int stride = (int)((size_t)stride_words * 4 / esz);
     int tpb = 64;
-    while (tpb > 1 && (size_t)tpb * (size_t)(cmax + 1) * 4 > 65536)
+    while (tpb > 1 && (size_t)tpb * (size_t)stride * esz > 65536)
         tpb >>= 1;
     const int64_t blocks = (a.nq + tpb - 1) / tpb;
-    hipLaunchKernelGGL(sw_topk_kernel, dim3((unsigned)blocks), dim3(tpb), (size_t)tpb * (size_t)(cmax + 1) * 4, stream,
-                       a);
+    if (small)
+        hipLaunchKernelGGL((sw_topk_kernel<uint16_t, 8>), dim3((unsigned)blocks), dim3(tpb), (size_t)tpb * stride * esz,
+                           stream, a, stride);
+    else
+        hipLaunchKernelGGL((sw_topk_kernel<uint32_t, 16>), dim3((unsigned)blocks), dim3(tpb), (size_t)tpb * stride * esz,
+                           stream, a, stride);
     DRM_HIP_CHECK(hipGetLastError());
 }
 
