@@ -545,16 +545,21 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         }
         __syncthreads();
         const int lead = lead_s, qe = qe_s;
-        for (int e = tid; e < PPROF; e += 64) {
-            const int ka = e / GST, kb = (e % GST) / PST, j = (e % GST) % PST;
-            uint32_t word = 0;
-            if (kb < 5 && j < qe && j < LQ) {
-                const int c = qbuf[lead + j];
-                // the diagonal term: +2 on a match (the -1 every cell takes makes it +1)
-                const uint32_t t = 0x0002u;
-                word = (c == acgt_byte(ka) ? t : 0u) | (c == acgt_byte(kb) ? t << 16 : 0u);
-            }
-            pprof[e] = word;
+        // one column per lane: its query byte is tested once against A, C, G, T and written to the 25 rows; the words
+        // between row blocks (GST - 5 * PST) are never read
+        for (int j = tid; j < PST; j += 64) {
+            const int c = (j < qe && j < LQ) ? (int)qbuf[lead + j] : -1; // past the query: matches nothing
+            // the diagonal term: +2 on a match (the -1 every cell takes makes it +1); code 4 matches nothing
+            uint32_t m[5];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                m[k] = c == acgt_byte(k) ? 0x0002u : 0u;
+            m[4] = 0u;
+#pragma unroll
+            for (int ka = 0; ka < 5; ++ka)
+#pragma unroll
+                for (int kb = 0; kb < 5; ++kb)
+                    pprof[ka * GST + kb * PST + j] = m[ka] | (m[kb] << 16);
         }
         __syncthreads();
         // longer than the buffer: unsupported here (-3); more than LQ columns left after the tags: the bit-profile
