@@ -31,7 +31,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-CLOCK_HZ = 2.4e9       # MI355X_MICROARCH.md: max engine clock 2400 MHz
+# dependent-load latency of the search's pointer chase (a random 384-B row behind a random 384-B row), measured by
+# tools/microbench/memlat.hip on an MI355X box (profiles/r03/box_diag_A.txt); the latency floor of roofline uses it
+DEP_LOAD_LATENCY_S = 1.08e-6
+SEARCH_LUT_BYTES = 8 * 256 * 4  # the lean search kernel's LDS per resident query (PQ 8 x 8 LUT)
 SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, false>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline rows) launch (hnsw_pq_fast.hip)
 FLAT_KERNEL = "hnsw_flat_search_kernel<16, 0, false, 0>"  # --index flat: what C3 (d = 128, ef = 128) launches
 SW_KERNEL = "sw_score_f16_kernel<150>"  # 150 DP columns: a tagged 150 bp read without its "<" / ">" ends
@@ -73,15 +76,16 @@ def committed_pmc(kernel_substr, workload):
 VALU_CYC = 2.4  # cycles per wave64 32-bit VALU instruction per SIMD at >= 4 waves (profiles/r02/valu_rate_probe.txt)
 
 
-def issue_ceiling(pmc, hops, ms):
+def issue_ceiling(pmc, hops, ms, ncu, clock_hz):
     """Issue-bound ceiling of the search kernel from its committed PMC counters: wave-instructions per
-    hop, and the launch time the VALU stream alone (1024 SIMDs at VALU_CYC cycles per instruction) and
-    the scalar stream alone (one scalar unit per CU, 256 CUs, one instruction per cycle) would take."""
+    hop, and the launch time the VALU stream alone (4 SIMDs per CU at VALU_CYC cycles per instruction) and
+    the scalar stream alone (one scalar unit per CU, one instruction per cycle) would take; CU count and clock are
+    the device's (drm_device_get_props)."""
     if not pmc or "SQ_INSTS_VALU" not in pmc or hops <= 0:
         return None
     v, sc, lds = pmc["SQ_INSTS_VALU"], pmc.get("SQ_INSTS_SALU", 0.0), pmc.get("SQ_INSTS_LDS", 0.0)
-    valu_ms = v * VALU_CYC / (1024 * CLOCK_HZ) * 1e3
-    salu_ms = sc / (256 * CLOCK_HZ) * 1e3
+    valu_ms = v * VALU_CYC / (4 * ncu * clock_hz) * 1e3
+    salu_ms = sc / (ncu * clock_hz) * 1e3
     return {"valu_per_hop": round(v / hops, 1), "salu_per_hop": round(sc / hops, 1), "lds_per_hop": round(lds / hops, 1),
             "valu_bound_ms": round(valu_ms, 2), "salu_bound_ms": round(salu_ms, 2),
             "frac_of_issue_ceiling": round(max(valu_ms, salu_ms) / ms, 3),
@@ -370,12 +374,13 @@ def host_path(ix, table, q_emb, queries, K, EF, flat):
             "note": "drm_search_rerank, pinned host in/out, one rank, PCIe-inclusive (not the metric)"}
 
 
-def gather_results(D, dev, n_total, bufs, local_host):
+def gather_results(D, dev, n_total, bufs):
     """End-of-run exchange: every rank's device-resident result rows are gathered to
     rank 0 over RCCL by the library's own C++ path (drm_comm_gather_rows: grouped ncclSend/ncclRecv over
-    xGMI), outside the timed region; the RCCL unique id travels over the gloo control plane. Rank 0
-    checks its own shard in the gathered rows. An exception is returned as {"error": ...}: gather_verdict
-    turns it into a failed job."""
+    xGMI), after the timed region. Verification (shard_checksums): every rank checksums its own rows on the device
+    (drm_device_checksum, position-dependent), rank 0 checksums each rank's row range of the gathered buffers on the
+    device, and the sums are compared over the gloo control plane -- every rank's shard is checked and nothing is
+    copied to the host. An exception is returned as {"error": ...}: gather_verdict turns it into a failed job."""
     if D.world == 1:
         return None
     from deepreadmapper_amd.device import device_count
@@ -385,7 +390,6 @@ def gather_results(D, dev, n_total, bufs, local_host):
     try:
         from deepreadmapper_amd.device import DeviceBuffer, synchronize
         from deepreadmapper_amd.executor import Comm
-        from deepreadmapper_amd.shard import shard_range
         if D.comm is None:
             obj = [Comm.unique_id() if D.rank == 0 else None]
             D.dist.broadcast_object_list(obj, src=0)
@@ -402,14 +406,26 @@ def gather_results(D, dev, n_total, bufs, local_host):
         synchronize()
         ms = (time.perf_counter() - t0) * 1e3
         out = {"backend": "RCCL (drm_comm_gather_rows, C++)", "ms": round(ms, 3), "bytes_per_rank": int(nbytes)}
+        local = {name: b.checksum() for name, b in bufs}
+        match = shard_checksums(D, n_total, local, lambda lo, hi: {k: v.checksum(lo, hi) for k, v in full.items()})
         if D.rank == 0:
-            lo, hi = shard_range(n_total, 0, D.world)
-            out["rank0_shard_matches"] = bool(all(np.array_equal(full[k].download()[lo:hi], v)
-                                                  for k, v in local_host.items()))
+            out["shards_match"] = match
             out["rows"] = int(n_total)
         return out
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+def shard_checksums(D, n_total, local_sums, slice_sums):
+    """Every rank's checksums of its own result rows (local_sums: {buffer: sum}) against rank 0's checksums of that
+    rank's row range [lo_r, hi_r) of the gathered buffers (slice_sums(lo, hi) -> {buffer: sum}), exchanged over the
+    gloo control plane. Returns rank 0's list of per-rank matches (None on the other ranks)."""
+    from deepreadmapper_amd.shard import shard_range
+    sums = [None] * D.world
+    D.dist.all_gather_object(sums, local_sums)
+    if D.rank != 0:
+        return None
+    return [slice_sums(*shard_range(n_total, r, D.world)) == sums[r] for r in range(D.world)]
 
 
 def gather_verdict(D, gather):
@@ -421,7 +437,7 @@ def gather_verdict(D, gather):
         return None
     skipped = gather is not None and "skipped" in gather
     bad = not skipped and (gather is None or "error" in gather or
-                           (D.rank == 0 and not gather.get("rank0_shard_matches", False)))
+                           (D.rank == 0 and not all(gather.get("shards_match") or [False])))
     n_bad = D.allreduce(1.0 if bad else 0.0, "SUM")
     n_skip = D.allreduce(1.0 if skipped else 0.0, "SUM")
     if n_bad > 0:
@@ -540,9 +556,6 @@ def main():
     ap.add_argument("--no-host-path", action="store_true", help="skip the pinned-host drm_search_rerank timing")
     ap.add_argument("--no-encoder", action="store_true", help="skip the GRU read-encoder timing")
     ap.add_argument("--no-l2", action="store_true", help="skip the L2 rerank (post_process_l2_static) timing")
-    ap.add_argument("--co", action="store_true", help="co-scheduled step (drm_search_rerank_device: search(b) beside "
-                                                       "SW rerank(b-1) on the same CUs) instead of search all, then SW all; "
-                                                       "measured no faster at C5 (DESIGN.md sec. 5)")
     ap.add_argument("--embed", choices=["kmer3", "gru"], default=None,
                     help="embeddings of windows and reads: gru (default for c5: the reference's GRU model, run on the "
                          "GPU by drm_vectorize) or kmer3 (the deterministic 3-mer stand-in; default for c3/c4)")
@@ -565,7 +578,7 @@ def main():
     if args.workload == "c4":
         return run_c4(args, D)
     from deepreadmapper_amd import synth
-    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream, device_count, set_device, synchronize
+    from deepreadmapper_amd.device import DeviceBuffer, Event, Stream, device_count, device_props, set_device, synchronize
     from deepreadmapper_amd.shard import shard_range
     from deepreadmapper_amd.search import HnswPqIndex
     from deepreadmapper_amd.rerank import WindowTable
@@ -612,20 +625,7 @@ def main():
     d_nd, d_nh, d_nu = DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32), DeviceBuffer(Q, np.int32)
     d_sc, d_id, d_st = DeviceBuffer((Q, K), np.int32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
     stream = Stream()
-    co = args.co and not flat
-    pstats = []
-
     def step(ev=None):
-        if co:
-            # drm_search_rerank_device: the search of batch b beside the SW rerank of batch b-1 on the same CUs
-            # (exec.cpp); stats = per-step device span and summed launch spans (the call synchronises)
-            from deepreadmapper_amd.executor import search_rerank_device
-            st = search_rerank_device(ix, table, d_x, Q, d_q, d_ql, queries.shape[1], d_D, d_I, d_sc, d_id, d_st, k=K,
-                                      ef=EF, d_ndis=d_nd, d_nhops=d_nh, d_nhops_upper=d_nu, stream=stream,
-                                      stats=ev is not None)
-            if ev is not None:
-                pstats.append(st)
-            return
         if ev:
             ev[0].record(stream)
         if flat:
@@ -655,33 +655,19 @@ def main():
     elapsed = time.perf_counter() - t0
     D.barrier()
     elapsed_max = D.allreduce(elapsed, "MAX")
-    if co:
-        # search / SW: summed launch spans of the step (overlapped with each other); the search roofline uses the
-        # average search launch, the figure rocprofv3 reports per dispatch
-        n_batches = pstats[0].n_batches
-        search_ms = float(np.mean([p.search_ms for p in pstats]))
-        sw_ms = float(np.mean([p.sw_ms for p in pstats]))
-        span_ms = float(np.mean([p.kernel_ms for p in pstats]))
-        first_search_ms = float(np.mean([p.first_search_ms for p in pstats]))
-        last_sw_ms = float(np.mean([p.last_sw_ms for p in pstats]))
-    else:
-        n_batches = 1
-        search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
-        sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
-        span_ms = search_ms + sw_ms
-        first_search_ms, last_sw_ms = search_ms, sw_ms
+    search_ms = float(np.mean([e[0].elapsed_ms(e[1]) for e in events]))
+    sw_ms = float(np.mean([e[1].elapsed_ms(e[2]) for e in events]))
+    span_ms = search_ms + sw_ms
     if os.environ.get("DRM_BENCH_VERBOSE"):
-        if co:
-            print("per-step span ms", [round(p.kernel_ms, 2) for p in pstats], "search", [round(p.search_ms, 2) for p in
-                  pstats], "sw", [round(p.sw_ms, 2) for p in pstats], file=sys.stderr, flush=True)
-        else:
-            print("per-step search ms", [round(e[0].elapsed_ms(e[1]), 2) for e in events],
-                  "sw ms", [round(e[1].elapsed_ms(e[2]), 2) for e in events], file=sys.stderr, flush=True)
+        print("per-step search ms", [round(e[0].elapsed_ms(e[1]), 2) for e in events],
+              "sw ms", [round(e[1].elapsed_ms(e[2]), 2) for e in events], file=sys.stderr, flush=True)
 
     # correctness / quality of this rank's last step
     if flat and ix.overflows():
         raise SystemExit(f"{ix.overflows()} queries outgrew the GPU candidate heap")
-    n_fallback = ix.fallbacks()
+    n_err = ix.search_errors()  # queries past the hop bound / waves past the item bound
+    if n_err:
+        raise SystemExit(f"{n_err} search errors (hop / work-item bounds): search state broken")
     st = d_st.download()
     if not (st == K).all():
         raise SystemExit(f"rerank status != K for {(st != K).sum()} queries")
@@ -720,12 +706,15 @@ def main():
         bytes_q = 4 * info.d + l0 * deg0 * 4 + nup * info.M_hnsw * 4 + ndis * code + K * 12
         codebook = info.pq_M * (1 << info.pq_nbits) * (info.d // info.pq_M) * 4
         bytes_launch = float(bytes_q.sum() + codebook)
-    # per launch: the step's search runs as n_batches launches of ~Q / n_batches queries
-    avg_launch_ms = search_ms / n_batches
     achieved = bytes_launch / (search_ms * 1e-3) / 1e9
-    # the first batch's search runs alone on the device at full occupancy
-    first_bytes = float(bytes_q[:Q // n_batches].sum()) + (0.0 if flat else float(codebook))
-    achieved_alone = first_bytes / (first_search_ms * 1e-3) / 1e9
+    # the device, read at run time: the issue ceilings below use its CU count and peak engine clock
+    props = device_props(dev)
+    ncu, clock_hz = props["cu_count"], props["clock_hz"]
+    # latency floor of the pointer chase: every hop (upper or level 0) waits for one dependent row load, and a CU
+    # holds lds_per_cu / LUT queries in flight (20 at 160 KB / 8 KB), so no schedule of this design finishes sooner
+    # than hops / (CUs x queries per CU) x the dependent-load latency
+    q_per_cu = max(1, props["lds_per_cu"] // SEARCH_LUT_BYTES) if not flat else None
+    lat_floor_ms = (float(nhops.sum()) / (ncu * q_per_cu) * DEP_LOAD_LATENCY_S * 1e3) if not flat else None
     cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
     pkey = args.workload + ("_flat" if flat else "") + ("_gru" if args.embed == "gru" else "")
@@ -734,14 +723,13 @@ def main():
     if pmc and "hbm_bytes_est" in pmc:
         traffic = float(pmc["hbm_bytes_est"])
     sw_prof_path, sw_pmc = committed_pmc(SW_KERNEL, pkey)
-    ncu = int(os.environ.get("DRM_CU_COUNT", "256"))
     sw_gcups = cells / (sw_ms * 1e-3) / 1e9
     # SW roofline = the hardware's VALU issue rate: 4 SIMDs per CU, each issuing one wave64 VALU instruction per 4
     # cycles (packed 16-bit) or per 2 cycles (32-bit). Instructions per launch: the committed PMC count of this
     # workload's SW kernel when there is one (SQ_INSTS_VALU per dispatch), else the static DP count (one wave
     # instruction advances 64 lanes x 2 candidates by one cell; 3.51 per cell pair); issue cycles = instructions x
     # the DP block's average cycles per instruction (SW_ISSUE_CYC_PER_VALU)
-    sw_peak_cyc = ncu * 4 * CLOCK_HZ
+    sw_peak_cyc = ncu * 4 * clock_hz
     # the DP's own cells: the tags of the 152-byte queries are not DP columns (sw_rerank.hip)
     dp_cells = float(Q) * K * refs.shape[1] * max(queries.shape[1] - 2, 1)
     sw_instr_static = dp_cells / 128.0 * SW_VALU_PER_CELL_PAIR
@@ -750,7 +738,7 @@ def main():
         sw_instr, sw_instr_src = float(sw_pmc["SQ_INSTS_VALU"]), f"{sw_prof_path}: SQ_INSTS_VALU per dispatch"
     sw_achieved_cyc = sw_instr * SW_ISSUE_CYC_PER_VALU / (sw_ms * 1e-3)
     # the whole rerank's time (scoring, top-k, flagged re-scores) per DP cell pair per SIMD, against the mix floor
-    sw_cyc_pair = (sw_ms * 1e-3) * CLOCK_HZ * ncu * 4 / (dp_cells / 2.0 / 64.0)
+    sw_cyc_pair = (sw_ms * 1e-3) * clock_hz * ncu * 4 / (dp_cells / 2.0 / 64.0)
 
     host = None if args.no_host_path else host_path(ix, table, q_emb, queries, K, EF, flat)
     enc = None if args.no_encoder else encoder_timing(d_q, Q, queries.shape[1], dev)
@@ -760,7 +748,7 @@ def main():
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
     gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_L if flat else d_I),
-                                           ("search_dists", d_D)], {"sw_ids": ids})
+                                           ("search_dists", d_D)])
     gather_ok = gather_verdict(D, gather)
     result = None
     if D.rank == 0:
@@ -784,18 +772,23 @@ def main():
                        "parallelism": f"dp{N} (query shards, index replicated per GPU)"},
             "roofline": {"bound": "hbm", "kernel": search_kernel, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "bytes_per_launch": bytes_launch,
-                         "bytes_per_launch_avg": bytes_launch / n_batches, "launches_per_step": n_batches,
-                         "avg_launch_ms": round(avg_launch_ms, 4),
-                         "alone": {"frac": round(achieved_alone / HBM_PEAK_GBS, 5), "achieved": round(achieved_alone, 2),
-                                   "launch_ms": round(first_search_ms, 4),
-                                   "note": "the step's first search launch, alone on the device (full grid)"},
+                         "traffic": traffic, "bytes_per_launch": bytes_launch, "avg_launch_ms": round(search_ms, 4),
+                         "latency_floor_ms": round(lat_floor_ms, 2) if lat_floor_ms else None,
+                         "frac_of_latency_floor": round(lat_floor_ms / search_ms, 3) if lat_floor_ms else None,
+                         "hbm_frac_at_latency_floor": round(bytes_launch / (lat_floor_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if lat_floor_ms else None,
+                         "latency_floor_note": (f"{float(nhops.sum()):.4g} hops / ({ncu} CUs x {q_per_cu} queries in "
+                                                f"flight per CU, the LDS limit at {SEARCH_LUT_BYTES} B of LUT each) x "
+                                                f"{DEP_LOAD_LATENCY_S * 1e6:.2f} us dependent-load latency "
+                                                "(profiles/r03/box_diag_A.txt): the pointer chase's floor; frac is read "
+                                                "against it") if lat_floor_ms else None,
+                         "device": {"cu_count": ncu, "clock_hz": clock_hz, "arch": props["arch"]},
                          "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch, gfx950 x2 "
                                             "read correction, uncalibrated for 4-8 B random reads")
                          if traffic is not None else None,
                          "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
                          if pmc and "valu_issue_frac" in pmc else None,
-                         "issue": issue_ceiling(pmc, float(nhops.sum()), search_ms)},
+                         "issue": issue_ceiling(pmc, float(nhops.sum()), search_ms, ncu, clock_hz)},
             "sw_roofline": {"bound": "valu", "kernel": SW_KERNEL, "achieved": round(sw_achieved_cyc / 1e9, 2),
                             "peak": round(sw_peak_cyc / 1e9, 2), "unit": "G SIMD VALU-issue cycles/s",
                             "frac": round(sw_achieved_cyc / sw_peak_cyc, 4), "instr_per_launch": sw_instr,
@@ -803,7 +796,7 @@ def main():
                             "valu_per_cell_pair": round(SW_VALU_PER_CELL_PAIR, 3),
                             "issue_cycles_per_cell_pair": round(SW_VALU_PER_CELL_PAIR * SW_ISSUE_CYC_PER_VALU, 2),
                             "note": "frac = VALU issue cycles used (packed 16-bit 4, 32-bit 2 cycles per wave64 "
-                                    "instruction) / the SIMDs' capacity (1,024 SIMDs x 2.4 GHz); the DP's op count per "
+                                    "instruction) / the SIMDs' capacity (4 x the device's CUs x its peak clock); the DP's op count per "
                                     "cell pair is reported separately",
                             "mix_floor": {"rerank_cycles_per_cell_pair": round(sw_cyc_pair, 2),
                                           "floor_cycles_per_cell_pair_2_waves": round(SW_MIX_CYC_PER_PAIR[2], 2),
@@ -819,16 +812,13 @@ def main():
             "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
             if enc else None,
             "l2_rerank": l2,
-            "breakdown": {"schedule": (f"co-scheduled: {n_batches} batches, search(b) beside SW rerank(b-1) on the same "
-                                       f"CUs (drm_search_rerank_device)") if co else "sequential: search, then SW rerank",
+            "breakdown": {"schedule": "sequential: search, then SW rerank, each with the whole chip",
                           "device_span_ms": round(span_ms, 3),
                           "search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),
-                          "first_search_alone_ms": round(first_search_ms, 3), "last_sw_alone_ms": round(last_sw_ms, 3),
                           "sw_gcups": round(cells / (sw_ms * 1e-3) / 1e9, 1),
                           "ndis_mean": round(float(ndis.mean()), 1), "nhops_mean": round(float(nhops.mean()), 1),
                           "distances_computed_mean": round(float(ndis_computed.mean()), 1),
                           "bytes_per_query": round(float(bytes_q.mean()), 1),
-                          "tie_fallback_queries": n_fallback,
                           "truth_top1": round(top1, 4), "truth_in_topk": round(intop, 4)},
         }
         emit(result)

@@ -23,15 +23,15 @@ DRM_ERR_INTERNAL = -8
 # Every symbol include/drm_hip.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = [
     "drm_last_error", "drm_version", "drm_device_count", "drm_set_device", "drm_device_sync", "drm_malloc",
-    "drm_free", "drm_memset", "drm_memcpy_h2d", "drm_memcpy_d2h", "drm_stream_create", "drm_stream_destroy",
+    "drm_free", "drm_memset", "drm_device_checksum", "drm_device_get_props", "drm_memcpy_h2d", "drm_memcpy_d2h", "drm_stream_create", "drm_stream_destroy",
     "drm_stream_sync", "drm_event_create", "drm_event_destroy", "drm_event_record", "drm_stream_wait_event", "drm_event_elapsed_ms",
     "drm_index_load", "drm_index_free", "drm_index_get_info", "drm_search", "drm_search_device",
-    "drm_search_device_ex", "drm_search_fallbacks", "drm_sw_scores",
+    "drm_search_device_ex", "drm_index_search_errors", "drm_sw_scores",
     "drm_refs_create", "drm_refs_free", "drm_post_process_sw_static", "drm_post_process_sw_static_device",
     "drm_build_hnswpq", "drm_build_hnsw_flat", "drm_embed_kmer3", "drm_build_hnswpq_device",
     "drm_embed_kmer3_device",
     "drm_flat_index_load", "drm_flat_index_free", "drm_flat_index_get_info", "drm_flat_search",
-    "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_fallbacks",
+    "drm_flat_search_device", "drm_flat_search_overflows", "drm_flat_search_errors",
     "drm_refs_get_info", "drm_host_alloc", "drm_host_free", "drm_search_rerank", "drm_multi_create",
     "drm_multi_free", "drm_multi_get_index_info", "drm_multi_search_rerank", "drm_comm_unique_id", "drm_comm_init",
     "drm_comm_free", "drm_comm_gather_rows", "drm_refs_create_genome", "drm_refs_is_genome",
@@ -41,7 +41,7 @@ EXPORTS = [
     "drm_vectorize", "drm_vectorize_device", "drm_encoder_flags",
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
     "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
-    "drm_index_set_search_waves", "drm_refs_set_sw_waves", "drm_search_rerank_device",
+    "drm_index_set_search_waves", "drm_search_rerank_device",
     "drm_index_set_exact_stats",
 ]
 
@@ -102,6 +102,8 @@ def lib():
         "drm_malloc": (C.c_int, [C.POINTER(vp), sz]),
         "drm_free": (C.c_int, [vp]),
         "drm_memset": (C.c_int, [vp, C.c_int, sz]),
+        "drm_device_checksum": (C.c_int, [vp, C.c_int64, C.POINTER(C.c_uint64), vp]),
+        "drm_device_get_props": (C.c_int, [C.c_int, vp]),
         "drm_memcpy_h2d": (C.c_int, [vp, vp, sz]),
         "drm_memcpy_d2h": (C.c_int, [vp, vp, sz]),
         "drm_stream_create": (C.c_int, [C.POINTER(vp)]),
@@ -117,13 +119,12 @@ def lib():
         "drm_index_get_info": (C.c_int, [vp, C.POINTER(IndexInfo)]),
         "drm_index_set_search_waves": (C.c_int, [vp, i32]),
         "drm_index_set_exact_stats": (C.c_int, [vp, i32]),
-        "drm_refs_set_sw_waves": (C.c_int, [vp, i32]),
         "drm_search_rerank_device": (C.c_int, [vp, vp, vp, i64, i32, i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
                                                vp, vp, vp, vp, C.POINTER(PipelineStats)]),
         "drm_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "drm_search_device_ex": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),
-        "drm_search_fallbacks": (C.c_int, [vp, C.POINTER(i64)]),
+        "drm_index_search_errors": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_sw_scores": (C.c_int, [vp, vp, vp, vp, vp, vp, i64, vp]),
         "drm_refs_create": (C.c_int, [vp, i64, i32, i64, C.c_int, C.POINTER(vp)]),
         "drm_refs_free": (C.c_int, [vp]),
@@ -139,7 +140,7 @@ def lib():
         "drm_flat_search": (C.c_int, [vp, vp, i64, i32, i32, i32, vp, vp, C.POINTER(SearchStats)]),
         "drm_flat_search_device": (C.c_int, [vp, vp, i64, i32, i32, vp, vp, vp, vp, vp, vp]),
         "drm_flat_search_overflows": (C.c_int, [vp, C.POINTER(i64)]),
-        "drm_flat_search_fallbacks": (C.c_int, [vp, C.POINTER(i64)]),
+        "drm_flat_search_errors": (C.c_int, [vp, C.POINTER(i64)]),
         "drm_build_hnsw_flat": (C.c_int, [vp, i64, i32, i32, i32, i32, C.c_uint64, C.c_char_p]),
         "drm_embed_kmer3": (C.c_int, [vp, vp, vp, i64, i32, C.c_uint64, vp]),
         "drm_build_hnswpq_device": (C.c_int, [vp, i64, i32, i32, i32, i32, i32, C.c_double, C.c_uint64, C.c_int,

@@ -109,6 +109,8 @@ struct BuildArgs {
     int32_t *clear_list;
     int32_t clear_cap;
     uint32_t *counter;
+    uint32_t *errors;            // waves past item_bound + beams past hop_bound: the build fails (DRM_ERR_INTERNAL)
+    int64_t item_bound, hop_bound; // count (a batch's nodes) and n (each node is expanded once) unless a test lowers them
 };
 
 __device__ __forceinline__ uint32_t adc8(const float *lut, const uint8_t *codes, int32_t v)
@@ -139,10 +141,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     const int lane = lane_id();
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
+    int64_t taken = 0;
     for (;;) {
         const int qi = wave_next_item(a.counter, lane);
         if ((int64_t)qi >= a.count)
             break;
+        if (++taken > a.item_bound) { // more items than the batch holds: a broken work-queue fetch
+            if (lane == 0)
+                atomicAdd(a.errors, 1u);
+            break;
+        }
         const int32_t u = a.order[a.start + qi];
         build_lut_m8_ptr(a.x + (size_t)u * a.d, a.centroids, lut, lane);
         const int ul = a.levels[u];
@@ -173,11 +181,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             if (lane == 0)
                 W[0] = bpack(dcur, cur);
             int nw = 1, clear_n = 1;
+            int64_t hops = 0;
             if (lane == 0) {
                 atomicOr(&vis[cur >> 5], 1u << (cur & 31));
                 clr[0] = cur;
             }
             for (;;) {
+                if (++hops > a.hop_bound) { // every node is expanded at most once: the beam's state is broken
+                    if (lane == 0)
+                        atomicAdd(a.errors, 1u);
+                    break;
+                }
                 // the nearest unexpanded entry (W is sorted: the first one)
                 int s = -1;
 #pragma unroll
@@ -524,7 +538,7 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
     DevArr<uint32_t> dvis((size_t)slots * (size_t)vis_words);
     DRM_HIP_CHECK(hipMemset(dvis.p, 0, sizeof(uint32_t) * (size_t)slots * (size_t)vis_words));
     DevArr<int32_t> dclr((size_t)slots * clear_cap);
-    DevArr<uint32_t> dcounter(1);
+    DevArr<uint32_t> dcounter(2); // [0] work queue head, [1] error count
     const int ef = std::min(efc, 256);
     BuildArgs a{};
     a.x = d_x;
@@ -547,11 +561,20 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
     a.clear_list = dclr.p;
     a.clear_cap = clear_cap;
     a.counter = dcounter.p;
+    a.errors = dcounter.p + 1;
+    auto env_bound = [](const char *k, int64_t dflt) {
+        const char *e = std::getenv(k);
+        const int64_t v = e ? std::atoll(e) : 0;
+        return v > 0 ? std::min(v, dflt) : dflt;
+    };
+    a.hop_bound = env_bound("DRM_BUILD_HOP_BOUND", n);
+    DRM_HIP_CHECK(hipMemset(dcounter.p, 0, 2 * sizeof(uint32_t)));
     const size_t lds = sizeof(float) * 8 * 256;
     for (int64_t start = 1; start < n;) {
         const int64_t cnt = std::min(std::min(start, kMaxBatch), n - start);
         a.start = start;
         a.count = cnt;
+        a.item_bound = env_bound("DRM_BUILD_ITEM_BOUND", cnt);
         DRM_HIP_CHECK(hipMemsetAsync(dcounter.p, 0, sizeof(uint32_t), nullptr));
         const int grid = (int)std::min<int64_t>(cnt, slots);
         if (a.ef <= 128)
@@ -574,6 +597,11 @@ void build_hnswpq_gpu(const float *d_x, int64_t n, int d, int M_pq, int nbits, i
         }
     }
     DRM_HIP_CHECK(hipDeviceSynchronize());
+    uint32_t nerr = 0;
+    DRM_HIP_CHECK(hipMemcpy(&nerr, dcounter.p + 1, sizeof(nerr), hipMemcpyDeviceToHost));
+    if (nerr)
+        throw Error(DRM_ERR_INTERNAL, std::to_string(nerr) + " insertion waves exceeded their work-item or beam-hop "
+                                                             "bound: build state broken");
     if (verbose)
         std::fprintf(stderr, "[gpu build] graph built %.1fs\n", secs_since(t0));
     // 5. faiss layout

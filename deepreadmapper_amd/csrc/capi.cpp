@@ -69,6 +69,36 @@ template <class T> struct DevBuf { // RAII device buffer for host-pointer entry 
     void download(T *h) const { DRM_HIP_CHECK(hipMemcpy(h, p, sizeof(T) * n, hipMemcpyDeviceToHost)); }
 };
 
+// drm_device_checksum: sum over the 8-byte little-endian words w_i of a buffer (the tail zero-padded) of
+// splitmix64(w_i + i * 0x9E3779B97F4A7C15), mod 2^64 -- position-dependent, order-free, so a grid-stride sum with
+// one atomic per wave computes it (deepreadmapper_amd.device.host_checksum is the same function on the host)
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void checksum_kernel(const uint8_t *p, int64_t nbytes, unsigned long long *out)
+{
+    const int64_t nw = (nbytes + 7) >> 3;
+    uint64_t acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (int64_t)gridDim.x * 256) {
+        uint64_t w;
+        if (8 * i + 8 <= nbytes) {
+            w = reinterpret_cast<const uint64_t *>(p)[i];
+        } else {
+            w = 0;
+            for (int64_t b = 8 * i; b < nbytes; ++b)
+                w |= (uint64_t)p[b] << (8 * (b - 8 * i));
+        }
+        acc += mix64(w + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+    }
+    for (int o = 32; o > 0; o >>= 1)
+        acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
 template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 {
     T *p = nullptr;
@@ -85,7 +115,7 @@ void free_index(drm::DeviceIndex &d)
     if (d.trace)
         (void)hipHostFree(d.trace);
     void *ptrs[] = {d.centroids, d.codes,   d.nbr0,   d.upper_off, d.upper_nbr, d.visited,
-                    d.clear_list, d.counter, d.stamps,   d.fb_list,   d.log,       d.rows, d.upper_codes};
+                    d.clear_list, d.counter, d.stamps,   d.log,       d.rows,      d.upper_codes};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -100,6 +130,21 @@ int drm_version(void) { return 100; /* 0.1.0 */ }
 int drm_device_count(int *n)
 {
     return guarded([&] { DRM_HIP_CHECK(hipGetDeviceCount(n)); });
+}
+int drm_device_get_props(int device, drm_device_props *out)
+{
+    return guarded([&] {
+        if (!out)
+            throw Error(DRM_ERR_ARG, "null argument");
+        hipDeviceProp_t p;
+        DRM_HIP_CHECK(hipGetDeviceProperties(&p, device));
+        *out = drm_device_props{};
+        out->cu_count = p.multiProcessorCount;
+        out->clock_khz = p.clockRate;
+        out->total_mem = (int64_t)p.totalGlobalMem;
+        out->lds_per_cu = (int32_t)p.maxSharedMemoryPerMultiProcessor;
+        std::snprintf(out->arch, sizeof(out->arch), "%s", p.gcnArchName);
+    });
 }
 int drm_set_device(int device)
 {
@@ -123,6 +168,28 @@ int drm_free(void *ptr)
 int drm_memset(void *ptr, int value, size_t bytes)
 {
     return guarded([&] { DRM_HIP_CHECK(hipMemset(ptr, value, bytes)); });
+}
+int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *stream)
+{
+    return guarded([&] {
+        if (!out || nbytes < 0 || (nbytes > 0 && (!d_ptr || ((uintptr_t)d_ptr & 7u) != 0u)))
+            throw Error(DRM_ERR_ARG, "drm_device_checksum: needs an 8-byte aligned device pointer and an output");
+        hipStream_t s = (hipStream_t)stream;
+        unsigned long long *d_out = nullptr;
+        DRM_HIP_CHECK(hipMallocAsync((void **)&d_out, sizeof(*d_out), s));
+        DRM_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(*d_out), s));
+        const int64_t nw = (nbytes + 7) >> 3;
+        if (nw > 0) {
+            const int64_t blocks = std::min<int64_t>((nw + 255) / 256, 4096);
+            hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint8_t *)d_ptr, nbytes, d_out);
+            DRM_HIP_CHECK(hipGetLastError());
+        }
+        unsigned long long h = 0;
+        DRM_HIP_CHECK(hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, s));
+        DRM_HIP_CHECK(hipFreeAsync(d_out, s));
+        DRM_HIP_CHECK(hipStreamSynchronize(s));
+        *out = (uint64_t)h;
+    });
 }
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes)
 {
@@ -244,11 +311,11 @@ int drm_index_load(const char *path, int device, drm_index **out)
             }
         }
         d.upper_len = (int64_t)upper.size();
-        // tuning knobs: visited-set placement, kernel choice
-        if (const char *e = std::getenv("DRM_SEARCH_VMODE"))
-            d.vmode = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_EXACT"))
-            d.force_exact = std::atoi(e) ? 1 : 0;
+        // tuning knobs: kernel choice, occupancy, diagnostics; the safety bounds (tests lower them)
+        if (const char *e = std::getenv("DRM_SEARCH_HOP_BOUND"))
+            d.hop_bound = std::max<int64_t>(0, std::atoll(e));
+        if (const char *e = std::getenv("DRM_WAVE_ITEM_BOUND"))
+            d.item_bound = std::max<int64_t>(0, std::atoll(e));
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
         d.waves_per_cu_load = d.waves_per_cu;
@@ -260,8 +327,6 @@ int drm_index_load(const char *path, int device, drm_index **out)
             d.use_fast = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_INLINE"))
             d.use_inline = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
-            d.try_sorted = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
             d.force_lds_kernel = std::atoi(e) ? 1 : 0;
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
@@ -335,17 +400,18 @@ int drm_debug_search_trace(drm_index *index, uint32_t **ptr, int64_t *words)
     });
 }
 
-int drm_search_fallbacks(drm_index *index, int64_t *count)
+int drm_index_search_errors(drm_index *index, int64_t *count)
 {
     return guarded([&] {
         if (!index || !count)
             throw Error(DRM_ERR_ARG, "null argument");
-        uint32_t c[2] = {0, 0};
+        uint32_t c[4] = {0, 0, 0, 0};
         if (index->dev.counter) {
             DRM_HIP_CHECK(hipDeviceSynchronize());
             DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+            DRM_HIP_CHECK(hipMemset(index->dev.counter + 3, 0, sizeof(uint32_t)));
         }
-        *count = (int64_t)c[1];
+        *count = (int64_t)c[3];
     });
 }
 
@@ -471,7 +537,7 @@ void free_flat(drm::DeviceFlatIndex &d)
 {
     void *ptrs[] = {d.vec,        d.l0,         d.l0cnt,      d.up_off,    d.up,        d.labels,  d.visited,
                     d.clear_list, d.cand_ovf_k, d.cand_ovf_i, d.top_ovf_k, d.top_ovf_i, d.counter, d.stamps,
-                    d.fb_list};
+                    };
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -526,8 +592,10 @@ int drm_flat_index_load(const char *path, int device, drm_flat_index **out)
         }
         if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
             d.waves_per_cu = std::max(1, std::atoi(e));
-        if (const char *e = std::getenv("DRM_SEARCH_SORTED"))
-            d.try_sorted = std::atoi(e) ? 1 : 0;
+        if (const char *e = std::getenv("DRM_SEARCH_HOP_BOUND"))
+            d.hop_bound = std::max<int64_t>(0, std::atoll(e));
+        if (const char *e = std::getenv("DRM_WAVE_ITEM_BOUND"))
+            d.item_bound = std::max<int64_t>(0, std::atoll(e));
         if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
             if (std::atoi(e)) {
                 DRM_HIP_CHECK(hipMalloc(&d.stamps, 8 * sizeof(uint64_t)));
@@ -619,17 +687,18 @@ int drm_flat_search_overflows(drm_flat_index *index, int64_t *count)
     });
 }
 
-int drm_flat_search_fallbacks(drm_flat_index *index, int64_t *count)
+int drm_flat_search_errors(drm_flat_index *index, int64_t *count)
 {
     return guarded([&] {
         if (!index || !count)
             throw Error(DRM_ERR_ARG, "null argument");
-        uint32_t c[3] = {0, 0, 0};
+        uint32_t c[4] = {0, 0, 0, 0};
         if (index->dev.counter) {
             DRM_HIP_CHECK(hipDeviceSynchronize());
             DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+            DRM_HIP_CHECK(hipMemset(index->dev.counter + 3, 0, sizeof(uint32_t)));
         }
-        *count = (int64_t)c[2];
+        *count = (int64_t)c[3];
     });
 }
 
@@ -664,8 +733,13 @@ int drm_flat_search(drm_flat_index *index, const float *x, int64_t n, int32_t d,
         DRM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
-        uint32_t c[2] = {0, 0};
+        uint32_t c[4] = {0, 0, 0, 0};
         DRM_HIP_CHECK(hipMemcpy(c, index->dev.counter, sizeof(c), hipMemcpyDeviceToHost));
+        if (c[3]) {
+            DRM_HIP_CHECK(hipMemset(index->dev.counter + 3, 0, sizeof(uint32_t)));
+            throw Error(DRM_ERR_INTERNAL, std::to_string(c[3]) + " queries exceeded the search's hop bound or waves "
+                                                                 "their work-item bound: search state broken");
+        }
         if (c[1])
             throw Error(DRM_ERR_UNSUPPORTED, std::to_string(c[1]) + " queries outgrew the GPU candidate heap");
         dD.download(D);
@@ -795,15 +869,6 @@ int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, in
             *ref_len = refs->dev.ref_len;
         if (device)
             *device = refs->dev.device;
-    });
-}
-
-int drm_refs_set_sw_waves(drm_refs *refs, int32_t waves_per_cu)
-{
-    return guarded([&] {
-        if (!refs || waves_per_cu < 0)
-            throw Error(DRM_ERR_ARG, "invalid argument");
-        refs->dev.sw_waves_per_cu = waves_per_cu;
     });
 }
 

@@ -19,27 +19,11 @@
 
 namespace drm {
 
-// Large, randomly accessed device arrays (index rows and codes, visited bitmaps, window table). With
-// DRM_CONTIG (a mask of the kinds below) they are asked for as physically contiguous memory; plain
-// hipMalloc otherwise, or when the driver cannot. Measured: contiguous placement makes the C5 search
-// slower, so the default mask is 0.
+// Large, randomly accessed device arrays (index rows and codes, visited bitmaps, window table): plain hipMalloc.
+// (Physically contiguous placement, hipDeviceMallocContiguous, measured slower for the C5 search in round 3 and was
+// removed in round 5) The kind names what the allocation holds.
 enum BigKind { kBigIndex = 1, kBigVisited = 2, kBigWindows = 4 };
-inline hipError_t malloc_big(void **p, size_t bytes, BigKind kind)
-{
-    static const int mask = [] {
-        const char *e = std::getenv("DRM_CONTIG");
-        return e ? std::atoi(e) : 0;
-    }();
-    if ((mask & (int)kind) && bytes >= ((size_t)64 << 20)) {
-        const hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
-        if (std::getenv("DRM_CONTIG_LOG"))
-            std::fprintf(stderr, "[contig] %zu MiB: %s\n", bytes >> 20, e == hipSuccess ? "contiguous" : "fallback");
-        if (e == hipSuccess)
-            return hipSuccess;
-        (void)hipGetLastError();
-    }
-    return hipMalloc(p, bytes);
-}
+inline hipError_t malloc_big(void **p, size_t bytes, BigKind) { return hipMalloc(p, bytes); }
 
 constexpr int kMaxLevels = 24; // HNSW levels representable in SearchArgs::cum
 constexpr int64_t kTraceWords = 8 + 8 * (1 << 20); // diagnostic trace: a count, then 8-word records
@@ -52,9 +36,10 @@ struct DeviceIndex {
     int32_t deg0 = 0, n_levels = 0, max_level = -1, entry_point = -1;
     int32_t cum[kMaxLevels + 1] = {};
     int32_t has_dup_links = 0; // some neighbour row lists one id twice
-    int32_t vmode = 0;         // visited set: 0 = HBM bitmap, 1 = LDS hash (spills to the bitmap)
-    int32_t force_exact = 0;   // skip the sorted-array pass (every query through the exact kernel)
-    int32_t try_sorted = 0;    // run the sorted-array pass first (DRM_SEARCH_SORTED=1)
+    // safety bounds: a query past hop_bound level-0 hops, or a persistent wave past item_bound
+    // work items, ends with an error count (DRM_ERR_INTERNAL); 0 = the natural bounds (ntotal hops, n items), set
+    // lower only by tests (DRM_SEARCH_HOP_BOUND, DRM_WAVE_ITEM_BOUND, read at load)
+    int64_t hop_bound = 0, item_bound = 0;
     int32_t waves_per_cu = 20; // resident search waves per CU (LDS allows 20 at 8 KB of LUT each)
     int32_t waves_per_cu_load = 20; // the value set at load (DRM_SEARCH_WAVES_PER_CU or 20): what 0 restores
     int32_t exact_stats = 0;   // lean kernel: count faiss's ndis with a visited bitmap (DRM_SEARCH_EXACT_STATS)
@@ -81,9 +66,7 @@ struct DeviceIndex {
     uint32_t *visited = nullptr;   // [n_slots][vis_words]
     int32_t clear_cap = 0;
     int32_t *clear_list = nullptr; // [n_slots][clear_cap]
-    uint32_t *counter = nullptr;   // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] errors
-    int32_t *fb_list = nullptr;    // queries the sorted-array pass handed to the exact kernel
-    int64_t fb_cap = 0;
+    uint32_t *counter = nullptr;   // [0] work queue head, [3] error count (hop / item bounds)
     int32_t use_fast = 1;          // lean kernel (hnsw_pq_fast.hip) where it applies; DRM_SEARCH_FAST=0 off
     uint64_t *log = nullptr;       // [n_slots][log_cap] accepted pushes (lean kernel, k == ef)
     int32_t log_cap = 0, log_slots = 0;
@@ -117,14 +100,13 @@ struct SearchArgs {
     int64_t vis_words;
     int32_t *clear_list;
     int32_t clear_cap;
-    uint32_t *counter;     // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] error count
+    uint32_t *counter;     // work queue head
+    uint32_t *errors;      // queries past hop_bound + waves past item_bound (drm_search: DRM_ERR_INTERNAL)
+    int64_t hop_bound;     // level-0 hops per query (ntotal unless a test lowers it)
+    int64_t item_bound;    // work items per wave (n unless a test lowers it)
     int32_t check_dups;
     int32_t x_aligned16; // queries 16-B aligned: float4 loads in the LUT build
     uint64_t *stamps; // diagnostic section timers (DRM_SEARCH_STAMPS=1), else null
-    const int32_t *qlist;  // exact kernel, fallback pass: process qlist[0 .. *qcount) instead of 0 .. n
-    const uint32_t *qcount;
-    int32_t *fb_list;      // sorted-array kernel: queries handed to the exact kernel
-    uint32_t *fb_count;
     uint64_t *log;         // lean kernel: per-slot log of accepted MinimaxHeap pushes
     int32_t log_cap;
     const int32_t *rows;   // lean kernel, inline layout: [ntotal][row_words] ids + codes (DeviceIndex::rows)
@@ -141,8 +123,11 @@ void launch_hnsw_pq_fast(const SearchArgs &a, int slots, bool stamps, hipStream_
 void build_inline_rows(DeviceIndex &ix);
 
 void reserve_search_scratch(DeviceIndex &ix);
-// after a synchronised search: DRM_ERR_INTERNAL if a query of it ended on the hop bound (counter[3])
-void check_search_errors(const DeviceIndex &ix);
+// after a synchronised search: DRM_ERR_INTERNAL if a query of it ended on the hop bound or a wave on its item bound
+// (counter[3], reset once reported)
+void check_search_errors(DeviceIndex &ix);
+int64_t search_hop_bound(const DeviceIndex &ix);
+int64_t search_item_bound(const DeviceIndex &ix, int64_t n);
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream);
 void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
@@ -157,7 +142,7 @@ struct DeviceFlatIndex {
     int64_t ntotal = 0;
     int32_t has_dup_links = 0;
     int32_t waves_per_cu = 32;  // cap on resident search waves per CU (the kernel build sets the real one)
-    int32_t try_sorted = 0;    // DRM_SEARCH_SORTED=1: tie-free sorted-array pass first, exact pass after
+    int64_t hop_bound = 0, item_bound = 0; // as DeviceIndex (DRM_SEARCH_HOP_BOUND, DRM_WAVE_ITEM_BOUND)
     float *vec = nullptr;      // [ntotal][d] f32 (512-B rows at d = 128)
     uint32_t *l0 = nullptr;    // [ntotal][maxM0] level-0 links (512-B rows at maxM0 = 128)
     uint32_t *l0cnt = nullptr; // [ntotal] link counts
@@ -176,10 +161,7 @@ struct DeviceFlatIndex {
     int64_t top_ovf_cap = 0;        // top_candidates entries beyond the LDS part (large ef), per slot
     float *top_ovf_k = nullptr;
     uint32_t *top_ovf_i = nullptr;
-    uint32_t *counter = nullptr;    // [0] queue head, [1] candidate_set overflows, [2] handed-over
-                                    // queries, [3] queue head of the exact pass
-    int32_t *fb_list = nullptr;     // queries the tie-free pass handed to the exact pass
-    int64_t fb_cap = 0;
+    uint32_t *counter = nullptr;    // [0] queue head, [1] candidate_set overflows, [3] error count (bounds)
     uint64_t *stamps = nullptr;     // diagnostic: 8 section-cycle sums (DRM_SEARCH_STAMPS=1)
     int64_t device_bytes = 0;
     HnswFlatHost meta;              // header fields for drm_flat_index_get_info (arrays released)
@@ -208,7 +190,9 @@ struct FlatArgs {
     int64_t vis_words;
     int32_t *clear_list;
     int32_t clear_cap;
-    uint32_t *counter;     // [0] work queue head, [1] fallback count, [2] fallback queue head, [3] error count
+    uint32_t *counter;     // work queue head
+    uint32_t *errors;      // queries past hop_bound + waves past item_bound (drm_flat_search: DRM_ERR_INTERNAL)
+    int64_t hop_bound, item_bound;
     int32_t check_dups;
     int32_t cand_lds;
     float *cand_ovf_k;
@@ -219,10 +203,6 @@ struct FlatArgs {
     uint32_t *top_ovf_i;
     int64_t top_ovf_cap;
     uint64_t *stamps;     // diagnostic section timers (DRM_SEARCH_STAMPS=1)
-    const int32_t *qlist; // exact pass after the tie-free one: qlist[0 .. *qcount) instead of 0 .. n
-    const uint32_t *qcount;
-    int32_t *fb_list;     // tie-free pass: queries that met a distance tie
-    uint32_t *fb_count;
     uint32_t *overflow;   // candidate_set overflow count (counter[1])
 };
 
@@ -242,7 +222,6 @@ struct DeviceRefs {
     int32_t *ws_scores = nullptr;
     int32_t *ws_ncand = nullptr;
     size_t ws_elems = 0, ws_nq = 0;
-    int32_t sw_waves_per_cu = 0; // > 0: SW score grid capped at this many waves per CU (co-resident search)
     // dynamic lookup (use_dynamic, post_process_sw_dynamic): the genome string instead of a window
     // table; window id w is genome[w / 2 ..+ ref_len), reverse-complemented when w is odd
     uint8_t *genome = nullptr;

@@ -108,11 +108,11 @@ struct ExecCache {
     int32_t *h_stats = nullptr;
     int64_t h_stats_n = 0;
     // drm_search_rerank_device: per-batch timing events (search start/end, rerank start/end) and the join
-    std::vector<hipEvent_t> ev_ss, ev_se, ev_ws, ev_we;
+    std::vector<hipEvent_t> ev_ss, ev_se, ev_we;
     hipEvent_t join = nullptr;
     void reserve_events(size_t nb)
     {
-        for (auto *v : {&ev_ss, &ev_se, &ev_ws, &ev_we})
+        for (auto *v : {&ev_ss, &ev_se, &ev_we})
             while (v->size() < nb) {
                 hipEvent_t e;
                 HC(hipEventCreate(&e));
@@ -200,7 +200,7 @@ struct ExecCache {
         for (hipEvent_t e : {e0, e1, join})
             if (e)
                 (void)hipEventDestroy(e);
-        for (auto *v : {&ev_ss, &ev_se, &ev_ws, &ev_we})
+        for (auto *v : {&ev_ss, &ev_se, &ev_we})
             for (hipEvent_t e : *v)
                 (void)hipEventDestroy(e);
         for (hipStream_t s : {s_search, s_sw})
@@ -395,40 +395,20 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
         ex.drain();
         throw;
     }
+    int64_t nerr = 0; // a query past the hop bound has nhops = -1 and partial rows: fail the call
+    abi_check(drm_index_search_errors(index, &nerr));
+    if (nerr)
+        throw Error(DRM_ERR_INTERNAL, std::to_string(nerr) + " queries exceeded the search's hop bound or waves their "
+                                                            "work-item bound: search state broken");
     if (rr)
         check_status(status, n, k);
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// drm_search_rerank_device: the same search -> SW rerank on device-resident buffers, pipelined so that the two
-// kernels share every CU. The search is a persistent pointer chase that waits on memory ~70 % of the time
-// (DESIGN.md sec. 4.1); the SW DP is VALU-bound (sec. 4.4). Run one after the other, each fills the chip alone;
-// run beside each other with capped grids -- search co_search waves per CU (8 KB of LUT each), rerank co_sw waves
-// per CU (16 KB of LDS, 215 VGPRs: one per SIMD beside three search waves) -- the rerank's VALU stream fills
-// the issue slots the search leaves idle. Phase p runs search(p) beside rerank(p-1): s_search enqueues
-// search(p) behind rerank(p-2) and s_sw enqueues rerank(p-1) behind search(p-1), so both start together. The
-// first search and the last rerank run alone, with full grids.
-struct CoParams {
-    int batches, search_waves, sw_waves;
-};
-
-CoParams co_params(int64_t n)
-{
-    auto env = [](const char *k, int dflt) {
-        const char *e = std::getenv(k);
-        return e ? std::atoi(e) : dflt;
-    };
-    CoParams c;
-    // Default: one batch (the search, then the rerank, each with the whole chip). Measured at C5 (DESIGN.md
-    // sec. 5): a rerank wave alone on its SIMD issues at about half the SIMD's VALU rate (one wave issues every
-    // other cycle), so the rerank needs two waves per SIMD -- 2 x 240 of the 512 VGPRs -- and no search wave
-    // fits beside it; the best co-run (search 8 + rerank 4 waves per CU) matched the sequential step.
-    c.batches = std::max(1, env("DRM_CO_BATCHES", 1));
-    c.search_waves = env("DRM_CO_SEARCH_WAVES", 8);
-    c.sw_waves = env("DRM_CO_SW_WAVES", 4);
-    return c;
-}
-
+// drm_search_rerank_device: the same search -> SW rerank on device-resident buffers, on the caller's stream: the
+// search with the whole chip, then the rerank with the whole chip. (Round 3 ran search(b) beside rerank(b-1) on
+// shared CUs with capped grids; it measured slower at C5 -- a rerank wave alone on its SIMD issues at half rate
+// and no search wave fits beside two of them -- and was removed in round 5)
 void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, int64_t n, int32_t k_clusters,
                           int32_t ef, const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,
                           int64_t stride, int32_t k, float *d_D, int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops,
@@ -452,81 +432,26 @@ void search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, in
         throw Error(DRM_ERR_ARG, "index and window table live on different devices");
     HC(hipSetDevice(info.device));
     ExecCache &ex = exec_for(index, info.device);
-    const CoParams co = co_params(n);
-    const int P = co.batches;
-    ex.reserve_events((size_t)P);
+    ex.reserve_events(1);
     auto *pp = genome_mode ? drm_post_process_sw_dynamic_device : drm_post_process_sw_static_device;
-    const size_t kc = (size_t)k_clusters, kr = (size_t)k;
-    auto lo_of = [&](int b) { return n * b / P; };
-    const bool overlap = P > 1 && co.search_waves > 0 && co.sw_waves > 0;
-    // the grid caps are touched only when batches overlap (a caller's own setting is left alone otherwise)
-    auto search = [&](int b, int waves) {
-        const int64_t lo = lo_of(b), m = lo_of(b + 1) - lo;
-        if (overlap)
-            abi_check(drm_index_set_search_waves(index, waves));
-        HC(hipEventRecord(ex.ev_ss[(size_t)b], ex.s_search));
-        abi_check(drm_search_device_ex(index, d_x + (size_t)lo * info.d, m, k_clusters, ef, d_D + (size_t)lo * kc,
-                                       d_I + (size_t)lo * kc, d_ndis ? d_ndis + lo : nullptr,
-                                       d_nhops ? d_nhops + lo : nullptr, d_nhops_upper ? d_nhops_upper + lo : nullptr,
-                                       ex.s_search));
-        HC(hipEventRecord(ex.ev_se[(size_t)b], ex.s_search));
-    };
-    auto rerank = [&](int b, int waves) {
-        const int64_t lo = lo_of(b), m = lo_of(b + 1) - lo;
-        if (overlap)
-            abi_check(drm_refs_set_sw_waves(refs, waves));
-        HC(hipStreamWaitEvent(ex.s_sw, ex.ev_se[(size_t)b], 0));
-        HC(hipEventRecord(ex.ev_ws[(size_t)b], ex.s_sw));
-        abi_check(pp(refs, d_I + (size_t)lo * kc, m, k_clusters, d_queries + (size_t)lo * q_stride, d_q_len + lo,
-                      q_stride, stride, k, k_clusters, d_sw_scores + (size_t)lo * kr, d_sw_ids + (size_t)lo * kr,
-                      d_status + lo, ex.s_sw));
-        HC(hipEventRecord(ex.ev_we[(size_t)b], ex.s_sw));
-    };
-    try {
-        HC(hipEventRecord(ex.join, stream)); // both streams start behind the caller's earlier work
-        HC(hipStreamWaitEvent(ex.s_search, ex.join, 0));
-        HC(hipStreamWaitEvent(ex.s_sw, ex.join, 0));
-        for (int b = 0; b < P; ++b) {
-            if (b >= 2) // phase lock: search(b) starts beside rerank(b-1), after rerank(b-2)
-                HC(hipStreamWaitEvent(ex.s_search, ex.ev_we[(size_t)b - 2], 0));
-            search(b, (overlap && b > 0) ? co.search_waves : 0);
-            if (b >= 1)
-                rerank(b - 1, overlap ? co.sw_waves : 0);
-        }
-        rerank(P - 1, 0); // alone: the full grid
-        if (overlap) {
-            abi_check(drm_index_set_search_waves(index, 0));
-            abi_check(drm_refs_set_sw_waves(refs, 0));
-        }
-        HC(hipStreamWaitEvent(stream, ex.ev_se[(size_t)P - 1], 0));
-        HC(hipStreamWaitEvent(stream, ex.ev_we[(size_t)P - 1], 0));
-    } catch (...) {
-        if (overlap) {
-            (void)drm_index_set_search_waves(index, 0);
-            (void)drm_refs_set_sw_waves(refs, 0);
-        }
-        ex.drain();
-        throw;
-    }
+    HC(hipEventRecord(ex.ev_ss[0], stream));
+    abi_check(drm_search_device_ex(index, d_x, n, k_clusters, ef, d_D, d_I, d_ndis, d_nhops, d_nhops_upper, stream));
+    HC(hipEventRecord(ex.ev_se[0], stream));
+    abi_check(pp(refs, d_I, n, k_clusters, d_queries, d_q_len, q_stride, stride, k, k_clusters, d_sw_scores, d_sw_ids,
+                  d_status, stream));
+    HC(hipEventRecord(ex.ev_we[0], stream));
     if (stats) {
-        HC(hipEventSynchronize(ex.ev_we[(size_t)P - 1]));
-        HC(hipEventSynchronize(ex.ev_se[(size_t)P - 1]));
+        HC(hipEventSynchronize(ex.ev_we[0]));
         *stats = drm_pipeline_stats{};
         stats->nq = n;
-        stats->n_batches = P;
+        stats->n_batches = 1;
         float ms = 0.f;
-        for (int b = 0; b < P; ++b) {
-            HC(hipEventElapsedTime(&ms, ex.ev_ss[(size_t)b], ex.ev_se[(size_t)b]));
-            stats->search_ms += ms;
-            HC(hipEventElapsedTime(&ms, ex.ev_ws[(size_t)b], ex.ev_we[(size_t)b]));
-            stats->sw_ms += ms;
-        }
-        HC(hipEventElapsedTime(&ms, ex.ev_ss[0], ex.ev_we[(size_t)P - 1]));
-        stats->kernel_ms = ms;
         HC(hipEventElapsedTime(&ms, ex.ev_ss[0], ex.ev_se[0]));
-        stats->first_search_ms = ms;
-        HC(hipEventElapsedTime(&ms, ex.ev_ws[(size_t)P - 1], ex.ev_we[(size_t)P - 1]));
-        stats->last_sw_ms = ms;
+        stats->search_ms = stats->first_search_ms = ms;
+        HC(hipEventElapsedTime(&ms, ex.ev_se[0], ex.ev_we[0]));
+        stats->sw_ms = stats->last_sw_ms = ms;
+        HC(hipEventElapsedTime(&ms, ex.ev_ss[0], ex.ev_we[0]));
+        stats->kernel_ms = ms;
     }
 }
 

@@ -599,11 +599,6 @@ __device__ __forceinline__ int append_clear(const FlatArgs &a, int32_t *clr, int
     return clear_n + nf;
 }
 
-__device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false); // wave_shr:1
-}
-
 // Ascending (key, label) order of 128 pairs held as element i = lane + 64 r in register r: a bitonic
 // network, partners across lanes by ds_bpermute (j < 64) or within the lane (j = 64). Equal pairs
 // (only the +inf padding) may swap freely.
@@ -655,12 +650,14 @@ __device__ __forceinline__ void bitonic128(float (&k)[2], uint64_t (&l)[2])
         }                                                                                                   \
     } while (0)
 
-// NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path.
-// NR = 0: exact replay of both libstdc++ heaps (any input). NR > 0: tie-free fast path, see below.
+// NV = d / 8 when the query slice lives in registers (d = 128 -> 16), 0 for the generic LDS path. Both
+// libstdc++ heaps are replayed exactly (any input, ties included).
+// Bounded: a query past a.hop_bound level-0 hops, or a wave past a.item_bound work items, ends with an error count
+// (a.errors; drm_flat_search returns DRM_ERR_INTERNAL) instead of looping.
 // MODE 0: the whole search. MODE 1: the same with the common shape as compile-time constants
 // (d = 128, k = ef = 128, maxM0 = 128, maxM = 64, no repeated links, top heap fully in LDS): fewer
 // live SGPRs and no kernel-argument reloads in the hop loop.
-template <int NV, int NR, bool STAMPS, int MODE>
+template <int NV, bool STAMPS, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAVES))) void hnsw_flat_search_kernel(FlatArgs a_in)
 {
     FlatArgs a = a_in;
@@ -674,8 +671,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
         a.top_ovf_cap = 0;
         a.cand_lds = DRM_FLAT_CAND_LDS;
         a.check_dups = 0;
-        a.qlist = nullptr;
-        a.qcount = nullptr;
     }
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
@@ -697,15 +692,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
                              (DRM_GLOBAL float *)(a.cand_ovf_k + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap),
                              (DRM_GLOBAL uint32_t *)(a.cand_ovf_i + (size_t)blockIdx.x * (size_t)a.cand_ovf_cap)};
     const int cand_cap = a.cand_lds + (int)a.cand_ovf_cap;
-    // queue: 0 .. n-1, or (fallback pass) the *qcount query ids in qlist
-    const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
-
+    int64_t taken = 0;
     for (;;) {
-        int qi = wave_next_item(a.counter, lane);
-        if ((int64_t)qi >= nq)
+        const int qi = wave_next_item(a.counter, lane);
+        if ((int64_t)qi >= a.n)
             break;
-        if (a.qlist)
-            qi = __builtin_amdgcn_readfirstlane(a.qlist[qi]);
+        if (++taken > a.item_bound) { // more items than the queue holds: a broken work-queue fetch
+            if (lane == 0)
+                atomicAdd(a.errors, 1u);
+            break;
+        }
         float *Dq = a.D + (int64_t)qi * a.k;
         uint64_t *Lq = a.L + (int64_t)qi * a.k;
         if (a.ntotal == 0) {
@@ -777,130 +773,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
             if (a.clear_cap > 0)
                 clr[0] = (int32_t)cur;
         }
-        bool keep = true; // false: handed to the exact pass (NR > 0)
         int nres = 0;
-        if constexpr (NR > 0) {
-            // Tie-free fast path. While no two entries of top_candidates share a distance:
-            //  * top_candidates is a sorted array (entry e in register e >> 6 of lane e & 63), and
-            //    pop() drops its last entry -- there is one maximum, so the heap layout is moot;
-            //  * candidate_set holds exactly the entries of top not yet expanded, plus entries
-            //    evicted from top, whose distance then exceeds lowerBound for good (strictly, as the
-            //    evicted maximum was unique): they can only trigger `cdist > lowerBound`, which is
-            //    reached exactly when no unexpanded entry is left. So candidate_set.top() is the
-            //    first unexpanded entry (unique minimum), marked by bit 31 of its id once expanded.
-            // The first equal distance among top's entries hands the query to the exact pass.
-            float tk[NR];
-            uint32_t ti[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                tk[r] = INFINITY;
-                ti[r] = 0u;
-            }
-            if (lane == 0) {
-                tk[0] = curdist;
-                ti[0] = cur;
-            }
-            int tsz = 1;
-            float lb = curdist;
-            FLAT_STAMP(0); // query setup + upper levels
-            for (;;) {
-                int e = -1;
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const uint64_t m = bal(64 * r + lane < tsz && !(ti[r] >> 31));
-                    if (e < 0 && m)
-                        e = 64 * r + __builtin_ctzll(m);
-                }
-                if (e < 0)
-                    break;
-                uint32_t c = 0;
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    if ((e >> 6) == r) {
-                        c = __builtin_amdgcn_readlane(ti[r], e & 63);
-                        if (lane == (e & 63))
-                            ti[r] |= 0x80000000u;
-                    }
-                nhops++;
-                FLAT_STAMP(1); // next candidate
-                const int nf = expand_row(a, c, vis, fid, false, 0u, 0u);
-                FLAT_STAMP(2); // row + visited
-                l2_dispatch<NV>(a, q, qr, fid, nf, fd);
-                ndis += nf;
-                FLAT_STAMP(3); // distances
-                // consideration in link order: insert each accepted link by rank
-                for (int base = 0; base < nf && keep; base += 64) {
-                    const int f = base + lane;
-                    const float dl = f < nf ? fd[f] : INFINITY;
-                    const uint32_t il = f < nf ? fid[f] : 0u;
-                    uint64_t mask = bal(f < nf && (tsz < a.ef || lb > dl));
-                    while (mask) {
-                        const int b = __builtin_ctzll(mask);
-                        mask &= mask - 1;
-                        const float dist = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dl), b));
-                        if (!(tsz < a.ef || lb > dist))
-                            continue;
-                        const uint32_t id = __builtin_amdgcn_readlane(il, b);
-                        int rank = 0;
-                        uint64_t eq = 0;
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) {
-                            const bool valid = 64 * r + lane < tsz;
-                            rank += __popcll(bal(valid && tk[r] < dist));
-                            eq |= bal(valid && tk[r] == dist);
-                        }
-                        if (eq) {
-                            keep = false;
-                            break;
-                        }
-                        float nk[NR];
-                        uint32_t ni[NR];
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) {
-                            uint32_t sk = dpp_wave_shr1(__float_as_uint(tk[r]));
-                            uint32_t si = dpp_wave_shr1(ti[r]);
-                            if (r > 0 && lane == 0) {
-                                sk = __builtin_amdgcn_readlane(__float_as_uint(tk[r - 1]), 63);
-                                si = __builtin_amdgcn_readlane(ti[r - 1], 63);
-                            }
-                            const int ee = 64 * r + lane;
-                            nk[r] = ee < rank ? tk[r] : (ee == rank ? dist : __uint_as_float(sk));
-                            ni[r] = ee < rank ? ti[r] : (ee == rank ? id : si);
-                        }
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) {
-                            tk[r] = nk[r];
-                            ti[r] = ni[r];
-                        }
-                        if (tsz < a.ef)
-                            tsz++;
-#pragma unroll
-                        for (int r = 0; r < NR; ++r)
-                            if (((tsz - 1) >> 6) == r)
-                                lb = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(tk[r]), (tsz - 1) & 63));
-                    }
-                }
-                clear_n = append_clear(a, clr, clear_n, fid, nf);
-                __syncthreads();
-                FLAT_STAMP(4); // consideration
-                if (!keep)
-                    break;
-            }
-            if (keep) {
-                // no ties: the k smallest in ascending order are also the (dist, label) order
-                nres = min(tsz, a.k);
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const int ee = 64 * r + lane;
-                    if (ee < nres) {
-                        Dq[ee] = tk[r];
-                        Lq[ee] = a.labels[ti[r] & 0x7FFFFFFFu];
-                    }
-                }
-            } else if (lane == 0) {
-                a.fb_list[atomicAdd(a.fb_count, 1u)] = qi;
-            }
-        } else {
+        bool overrun = false;
+        {
             int top_len = 1, cand_len = 1;
             float lowerBound = curdist;
             bool overflow = false;
@@ -920,6 +795,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
             int slow_base = -1, slow_nf = 0;
             uint64_t slow_mask = 0;
             while (!slow && cand_len > 0) {
+                if (nhops - nhops_up > a.hop_bound) { // a node is expanded at most once: the bookkeeping is broken
+                    overrun = true;
+                    break;
+                }
                 const KV croot = kv_load(cdkv); // slot 0 is always in LDS
                 const float cdist = -__uint_as_float(__builtin_amdgcn_readfirstlane(croot.x));
                 if (cdist > lowerBound)
@@ -982,7 +861,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
                 __syncthreads();
                 FLAT_STAMP(4); // consideration: heap pushes / pops
             }
-            if (slow) {
+            if (slow && !overrun) {
                 ConsState st{top_len, cand_len, lowerBound, 0};
                 if (slow_base >= 0) { // the rest of the interrupted hop (its fresh links are still in LDS)
                     st = slow_consider(fd, fid, slow_nf, slow_base, slow_mask, st, top, cand, topkv, cdkv, a.ef,
@@ -990,6 +869,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
                     clear_n = append_clear(a, clr, clear_n, fid, slow_nf);
                 }
                 while (!st.overflow && st.cand_len > 0) {
+                    if (nhops - nhops_up > a.hop_bound) {
+                        overrun = true;
+                        break;
+                    }
                     const float cdist = -cand.key(0);
                     if (cdist > st.lb)
                         break;
@@ -1076,17 +959,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRM_FLAT_WAV
                 }
             }
         }
-        if (keep) {
-            for (int j = nres + lane; j < a.k; j += 64) {
-                Dq[j] = INFINITY;
-                Lq[j] = ~0ull;
-            }
-            if (lane == 0) {
-                a.ndis[qi] = ndis;
-                a.nhops[qi] = nhops;
-                if (a.nhops_upper)
-                    a.nhops_upper[qi] = nhops_up;
-            }
+        for (int j = nres + lane; j < a.k; j += 64) {
+            Dq[j] = INFINITY;
+            Lq[j] = ~0ull;
+        }
+        if (lane == 0) {
+            a.ndis[qi] = overrun ? -1 : ndis;
+            a.nhops[qi] = overrun ? -1 : nhops;
+            if (a.nhops_upper)
+                a.nhops_upper[qi] = nhops_up;
+            if (overrun)
+                atomicAdd(a.errors, 1u);
         }
         // VisitedTable reset: clear exactly the bits this query set
         // (no wait for these stores: VMEM completes in order, so the next query's first visited test,
@@ -1183,7 +1066,10 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.clear_list = ix.clear_list;
     a.clear_cap = ix.clear_cap;
     a.counter = ix.counter;
-    a.overflow = ix.counter + 1; // whichever queue head a pass uses
+    a.overflow = ix.counter + 1;
+    a.errors = ix.counter + 3;
+    a.hop_bound = ix.hop_bound > 0 ? std::min(ix.hop_bound, ix.ntotal) : ix.ntotal;
+    a.item_bound = ix.item_bound > 0 ? std::min(ix.item_bound, n) : n;
     a.check_dups = ix.has_dup_links;
     a.cand_lds = cand_lds;
     a.cand_ovf_k = ix.cand_ovf_k;
@@ -1195,59 +1081,22 @@ void launch_hnsw_flat_search(DeviceFlatIndex &ix, const float *d_x, int64_t n, i
     a.top_ovf_cap = ix.top_ovf_cap;
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 8 * sizeof(uint32_t), stream));
     a.stamps = ix.stamps;
-    a.qlist = nullptr;
-    a.qcount = nullptr;
-    // pass 1 (opt-in, DRM_SEARCH_SORTED=1): the tie-free sorted-array kernel (ef <= 256, d = 128,
-    // ids < 2^31); the queries that meet a distance tie go to fb_list and pass 2 (the exact heap
-    // replay) redoes them. Off by default: the 3-mer stand-in embedding maps shifted windows onto
-    // identical vectors so often that ~89 % of C3 queries meet a tie (oracle count).
-    const int nr = efc <= 64 ? 1 : efc <= 128 ? 2 : efc <= 256 ? 4 : 0;
-    const bool sorted_pass = ix.try_sorted && ix.d == 128 && nr > 0 && ix.ntotal < 0x7FFFFFFFll;
-    if (sorted_pass) {
-        if (n > ix.fb_cap) {
-            if (ix.fb_list)
-                DRM_HIP_CHECK(hipFree(ix.fb_list));
-            ix.fb_list = nullptr;
-            DRM_HIP_CHECK(hipMalloc(&ix.fb_list, sizeof(int32_t) * (size_t)n));
-            ix.fb_cap = n;
-        }
-        a.fb_list = ix.fb_list;
-        a.fb_count = ix.counter + 2;
-#define DRM_FLAT_SORTED(NR_)                                                                                   \
-    if (ix.stamps)                                                                                              \
-        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, NR_, true, 0>), dim3(slots), dim3(64), lds, stream, a);    \
-    else                                                                                                        \
-        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, NR_, false, 0>), dim3(slots), dim3(64), lds, stream, a);
-        if (nr == 1) {
-            DRM_FLAT_SORTED(1)
-        } else if (nr == 2) {
-            DRM_FLAT_SORTED(2)
-        } else {
-            DRM_FLAT_SORTED(4)
-        }
-#undef DRM_FLAT_SORTED
-        DRM_HIP_CHECK(hipGetLastError());
-        a.qlist = ix.fb_list;
-        a.qcount = ix.counter + 2;
-        a.counter = ix.counter + 3;
-        a.stamps = nullptr;
-    }
 #define DRM_FLAT_MAIN(M_)                                                                                      \
     if (ix.d == 128) {                                                                                          \
         if (a.stamps)                                                                                           \
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, true, M_>), dim3(slots), dim3(64), lds, stream, a); \
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, true, M_>), dim3(slots), dim3(64), lds, stream, a); \
         else                                                                                                    \
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<16, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
     } else {                                                                                                    \
         if (a.stamps)                                                                                           \
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, true, M_>), dim3(slots), dim3(64), lds, stream, a); \
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, true, M_>), dim3(slots), dim3(64), lds, stream, a); \
         else                                                                                                    \
-            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, 0, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
+            hipLaunchKernelGGL((hnsw_flat_search_kernel<0, false, M_>), dim3(slots), dim3(64), lds, stream, a); \
     }
     const bool fixed = ix.d == 128 && k == 128 && efc == 128 && ix.maxM0 == 128 && ix.maxM == 64 && top_lds == 129 &&
-                       !ix.has_dup_links && !a.stamps && !a.qlist && DRM_FLAT_Q_REGS;
+                       !ix.has_dup_links && !a.stamps && DRM_FLAT_Q_REGS;
     if (fixed)
-        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, 0, false, 1>), dim3(slots), dim3(64), lds, stream, a);
+        hipLaunchKernelGGL((hnsw_flat_search_kernel<16, false, 1>), dim3(slots), dim3(64), lds, stream, a);
     else {
         DRM_FLAT_MAIN(0)
     }

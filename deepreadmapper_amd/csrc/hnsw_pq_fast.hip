@@ -75,13 +75,11 @@ __device__ __forceinline__ uint64_t bperm64_addr(uint64_t v, uint32_t addr)
 }
 // a wave-uniform lane mask as this lane's predicate, with no per-lane arithmetic (the select uses the mask)
 __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
-// a > b for wave-uniform u64 keys, on the scalar unit (two 32-bit compares)
-__device__ __forceinline__ bool sgt64(uint64_t a, uint64_t b)
-{
-    const uint32_t ah = hi32(a), bh = hi32(b);
-    return ah > bh || (ah == bh && lo32(a) > lo32(b));
-}
 __device__ __forceinline__ int bitlen(uint32_t x) { return 32 - __builtin_clz(x); } // x >= 1
+__device__ __forceinline__ uint32_t dpp_rol1_u32(uint32_t v) // lane i <- lane i+1, lane 63 <- lane 0 (wave_rol:1)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x134, 0xF, 0xF, false);
+}
 __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // lane i <- lane i-1
 {
     const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp((int)hi32(old), (int)hi32(v), 0x138, 0xF, 0xF, false);
@@ -133,21 +131,22 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
 // ancestors whose path toward p takes the left child (2a + 1).
 struct PathConst {
     // every ancestor of any lane p (< 64) is below lane 32, so A's, Aup's and Lreq's high halves hold at most p
-    // itself: only the low halves are kept (three VGPRs), and p's own bit is checked against the ballot mask
-    uint32_t Alo, Auplo, Lreqlo;
-    // ds_bpermute byte addresses: this lane's left / right child lane (slots 2p+1, 2p+2 are held by lanes
-    // 2p+1, 2p+2 mod 64), and its parent in the chain of slot 127's ancestors (lane >> 1)
+    // itself: the low halves are kept, and Ahi is p's own bit for p >= 32 (0 below)
+    uint32_t Alo, Ahi, Auplo, Lreqlo;
+    // ds_bpermute byte addresses: this lane's left / right child lane (slots 2p+1, 2p+2 are held by lanes 2p+1, 2p+2
+    // mod 64), and its parent in the chain of slot 127's ancestors (lane >> 1)
     uint32_t addrL, addrR, addrHalf, half; // half = lane >> 1
-    // heap filling (push_fill): this lane's slots 2p+1, 2p+2 as 1-based positions 2p+2, 2p+3 share the bit
-    // length bl; their father is slot p, held by lane (p-1)/2 (the L half when p is odd; the root for p = 0)
-    uint32_t c2, bl, addrF;
+    // heap filling (push_fill): this lane's halves are the 1-based positions xL = 2p+2 and 2p+3 (lane 63's R: the root,
+    // position 1), both of bit length bl; their father is slot p, held by lane (p-1)/2 (its L half when p is odd, its
+    // R half when p is even) and, for p = 0, by lane 63's R (the root)
+    uint32_t xL, bl, addrF;
     // full-heap push: the chain index of this lane's L half on slot 127's ancestor chain (slot 127 = 0, 63 = 1, 31 = 2,
-    // 15 = 3, 7 = 4, 3 = 5, 1 = 6: lanes 63, 31, 15, 7, 3, 1, 0); 15 for every other lane
+    // 15 = 3, 7 = 4, 3 = 5, 1 = 6: lanes 63, 31, 15, 7, 3, 1, 0; the root, lane 63's R, is 7); 15 for every other lane
     uint32_t cidx;
     __device__ explicit PathConst(int lane)
         : addrL((uint32_t)((2 * lane + 1) & 63) << 2), addrR((uint32_t)((2 * lane + 2) & 63) << 2),
-          addrHalf((uint32_t)(lane >> 1) << 2), half((uint32_t)lane >> 1), c2(2u * (uint32_t)lane + 2u), bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)),
-          addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 0u),
+          addrHalf((uint32_t)(lane >> 1) << 2), half((uint32_t)lane >> 1), xL(2u * (uint32_t)lane + 2u),
+          bl((uint32_t)bitlen(2u * (uint32_t)lane + 2u)), addrF(lane > 0 ? (uint32_t)((lane - 1) >> 1) << 2 : 63u << 2),
           cidx(((lane + 1) & lane) == 0 ? 6u - (uint32_t)(31 - __builtin_clz((uint32_t)lane + 1u)) : 15u)
     {
         uint64_t A = 1ull << lane, Aup = 0, Lreq = 0;
@@ -160,20 +159,22 @@ struct PathConst {
             c = a;
         }
         Alo = (uint32_t)A;
+        Ahi = (uint32_t)(A >> 32);
         Auplo = (uint32_t)Aup;
         Lreqlo = (uint32_t)Lreq;
     }
-    // the lanes on the sift-down path: p and all its ancestors have mv set, and every ancestor chose the child
-    // toward p (lm: the nodes that take their L child)
+    // the lanes on the sift-down path: p and all its ancestors have mv set, and every ancestor chose the child toward
+    // p (lm: the nodes that take their L child). One per-lane test and one ballot, no scalar mask arithmetic.
     __device__ __forceinline__ uint64_t path(uint64_t mv, uint64_t lm) const
     {
-        return ballot(((uint32_t)mv & Alo) == Alo) & (mv | 0xFFFFFFFFull) & ballot(((uint32_t)lm & Auplo) == Lreqlo);
+        const uint32_t x = (~(uint32_t)mv & Alo) | (((uint32_t)lm ^ Lreqlo) & Auplo) | (~(uint32_t)(mv >> 32) & Ahi);
+        return ballot(x == 0u);
     }
 };
 
 // MinimaxHeap arrays (ef <= 128) in the sibling-pair layout. L / R are the faiss keys (a popped slot's id is -1
 // there, as in faiss's ids[] array); IL / IR hold each slot's node id, popped or not (-1: never filled), and move
-// with their keys through every sift. They are what the kernel's visited test reads.
+// with their keys through every sift. They are what the kernel's visited test reads. Lane 63's R / IR is the root.
 struct Heap {
     uint64_t L, R;
     int32_t IL, IR;
@@ -193,8 +194,15 @@ struct Heap {
         const int o = (s - 1) >> 1;
         return (s & 1) ? readlane32(IL, o) : readlane32(IR, o);
     }
-    // node v is in the heap (one compare per half, wave-uniform answer)
-    __device__ __forceinline__ bool holds(int32_t v) const { return (ballot(IL == v) | ballot(IR == v)) != 0ull; }
+    // node v is in the heap: one per-lane test (the smaller of the two id differences is 0) and one ballot
+    __device__ __forceinline__ bool holds(int32_t v) const
+    {
+        const uint32_t dl = (uint32_t)(IL ^ v), dr = (uint32_t)(IR ^ v);
+        return ballot((dl < dr ? dl : dr) == 0u) != 0ull;
+    }
+    // the root's key (high word) and node id
+    __device__ __forceinline__ uint32_t root_hi() const { return (uint32_t)__builtin_amdgcn_readlane((int)hi32(R), 63); }
+    __device__ __forceinline__ int32_t root_id() const { return readlane32(IR, 63); }
 
     // faiss heap_pop<CMax<float, int>>(k): slot k-1 sifted down from the root (1-based k >= 1).
     __device__ __forceinline__ void pop(int k, int lane)
@@ -284,20 +292,21 @@ struct Heap {
     }
 
     // heap_pop(128) then heap_push(128, vnew) on the full ef = 128 heap (MinimaxHeap::push when k == n), with the
-    // two cross-lane fetches issued together from the pre-pop registers: one ds_bpermute round trip per replace.
+    // cross-lane fetches issued together from the pre-pop registers: one ds_bpermute round trip per replace.
     //  * pop: slot 127 (lane 63's L) is sifted down from the root. Lane p on the path writes its chosen child slot
     //    with that child's own chosen child (chv of lane ch_p), or with slot 127's value when p is the path's last
-    //    node; the path is the set of lanes whose own and ancestors' chosen children move up (PathConst::path);
+    //    node; the path is the set of lanes whose own and ancestors' chosen children move up (PathConst::path). The
+    //    root (lane 63's R) takes node 0's chosen child when node 0 is on the path, else slot 127's value: lane 0
+    //    forms it and lane 63 takes it by one DPP wave rotate;
     //  * push: vnew enters slot 127 and climbs the chain of its ancestors (slots 63, 31, 15, 7, 3, 1: the L halves
     //    of lanes 31, 15, 7, 3, 1, 0; then the root). Chain holder c takes its father, slot c, whose post-pop value
     //    is lane c's own chv (or slot 127's value) if lane c >> 1 is on the path and took its L child, else its
-    //    pre-pop value: the only cross-lane part is the pre-pop fetch.
-    // Straight-line: every case is a lane mask (no branch), and lane 63's R (the root) is current on return. Returns
-    // the root after the push, its id in rootI.
-    __device__ __forceinline__ uint64_t replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int lane,
-                                                   int32_t &rootI)
+    //    pre-pop value; lane 0's father is the root.
+    // Straight-line, and every decision is a per-lane test on the vector unit (the scalar unit only counts h and
+    // combines two masks): the scalar-issue share of the hop is what bounds the kernel. The
+    // caller reads the new root from lane 63's R.
+    __device__ __forceinline__ void replace128(uint64_t vnew, int32_t vnewI, const PathConst &pc, int lane)
     {
-        constexpr uint64_t kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const uint64_t val = readlane64(L, 63); // slot 127
         const int32_t valI = readlane32(IL, 63);
         const uint64_t lm = ballot(L > R) | (1ull << 63); // node p takes its L child (node 63: slot 127 only)
@@ -314,20 +323,22 @@ struct Heap {
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
-        // per-lane tests, no scalar bit arithmetic: the path is a chain of nodes, so its deepest node p is the one
-        // with W >> p == 1
+        // per-lane tests: the path is a chain of nodes, so its deepest node p is the one with W >> p == 1
         const bool atlast = (W >> lane) == 1ull;
         const bool klast = (W >> pc.half) == 1ull;
         const bool moved = ((W & lm) >> pc.half) & 1ull; // lane (lane >> 1) is on the path and took its L child
-        const uint64_t c0 = readlane64(chv, 0);
-        const int32_t c0I = readlane32(chI, 0);
-        const bool r0 = (W & 1ull) != 0ull; // the root's larger child moves up
-        const uint64_t rootv = r0 ? c0 : val;
-        const int32_t rI = r0 ? c0I : valI;
-        // the chain's fathers after the pop (lane 0's is the root), from the pre-pop registers
+        // lane 0: the root after the pop -- node 0's chosen child if node 0 is on the path (lane 0's own bit of W),
+        // else slot 127's value
+        const bool onw = in_mask(W);
+        const uint64_t rootpp = onw ? chv : val;
+        const int32_t rootppI = onw ? chI : valI;
+        // the chain's fathers after the pop, from the pre-pop registers; lane 0's father is the root
+        const bool s1 = in_mask(1ull);
         uint64_t fl = moved ? (klast ? val : chv) : fpre;
         int32_t flI = moved ? (klast ? valI : chI) : fpreI;
-        // pop writes: the path nodes' chosen child slots
+        fl = s1 ? rootpp : fl;
+        flI = s1 ? rootppI : flI;
+        // pop writes: the path nodes' chosen child slots, and the root
         const uint64_t up = atlast ? val : up0;
         const int32_t upI = atlast ? valI : up0I;
         const bool wl = in_mask(W & lm), wr = in_mask(W & ~lm);
@@ -335,80 +346,58 @@ struct Heap {
         IL = wl ? upI : IL;
         R = wr ? up : R;
         IR = wr ? upI : IR;
-        // push: h = the chain's ancestors below vnew after the pop (lane 63 stands for the root)
         const bool s63 = in_mask(1ull << 63);
-        const uint64_t chain = s63 ? rootv : L;
-        const int h = __builtin_popcountll(ballot(vnew > chain) & kHold);
-        const bool s1 = in_mask(1ull);
-        fl = s1 ? rootv : fl;
-        flI = s1 ? rI : flI;
+        const uint64_t nroot = ((uint64_t)dpp_rol1_u32(hi32(rootpp)) << 32) | dpp_rol1_u32(lo32(rootpp)); // lane 63 <- lane 0
+        const int32_t nrootI = (int32_t)dpp_rol1_u32((uint32_t)rootppI);
+        R = s63 ? nroot : R;
+        IR = s63 ? nrootI : IR;
+        // push: h = the chain's ancestors below vnew after the pop (lane 63 stands for the root, index 7)
+        const uint64_t chain = s63 ? R : (pc.cidx < 15u ? L : ~0ull);
+        const uint32_t h = (uint32_t)__builtin_popcountll(ballot(vnew > chain));
         // the chain indices below h take their father's value, index h takes vnew (h = 7: the root)
-        const bool sh = pc.cidx < (uint32_t)h;
+        const bool sh = pc.cidx < h;
         L = sh ? fl : L;
         IL = sh ? flI : IL;
-        const bool xs = pc.cidx == (uint32_t)h;
+        const bool xs = pc.cidx == h;
         L = xs ? vnew : L;
         IL = xs ? vnewI : IL;
-        const uint64_t nroot = h == 7 ? vnew : rootv;
-        rootI = h == 7 ? vnewI : rI;
-        R = s63 ? nroot : R;
-        IR = s63 ? rootI : IR;
-        return nroot;
+        const bool xr = s63 && h == 7u;
+        R = xr ? vnew : R;
+        IR = xr ? vnewI : IR;
     }
 
-    // faiss heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128): val enters slot s = k - 1 and
-    // sifts up its ancestors, slot (k >> m) - 1 at chain index m (the root at m = bitlen(k) - 1). Lane-mask
-    // form: each lane tests whether one of its halves is on the chain (both halves share the index), the
-    // ancestors below val are a bottom prefix of length h (heap order), the slots of index < h take their
-    // father's value (one ds_bpermute per half), and the slot of index h takes val. The root is (rootv, rootI),
-    // also in lane 63's R / IR; returns the new root, its id in rootI.
-    __device__ __forceinline__ uint64_t push_fill(int k, uint64_t val, int32_t valI, const PathConst &pc, uint64_t rootv,
-                                                  int32_t &rootI)
+    // faiss heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128): val enters slot k - 1 and sifts up its
+    // ancestors. Lane-mask form: each half finds its chain index (1-based position x is on the chain of k at index
+    // m = bitlen(k) - bitlen(x) iff k >> m == x; lane 63's R, the root, is always on it, at index bitlen(k) - 1); the
+    // ancestors below val are a bottom prefix of length h (heap order), the halves of index < h take their father's
+    // value (one ds_bpermute round trip, issued first) and the half of index h takes val. No branch, no scalar
+    // bookkeeping: the root is not tracked here (the caller reads it once the heap is full).
+    __device__ __forceinline__ void push_fill(uint32_t k, uint64_t val, int32_t valI, const PathConst &pc)
     {
-        const uint32_t s1 = (uint32_t)k;
-        const int B = bitlen(s1);
-        const int m = B - (int)pc.bl;
-        const uint32_t t = m >= 0 ? (s1 >> m) : 0u;
-        const uint64_t OL = ballot(t == pc.c2), OR = ballot(t == pc.c2 + 1u); // this lane's half on the chain
-        const uint32_t sl = (s1 - 2u) >> 1;                                     // the lane of slot s
-        const uint64_t selfL = (s1 & 1u) ? 0ull : (1ull << sl), selfR = (s1 & 1u) ? (1ull << sl) : 0ull;
-        const int h = __builtin_popcountll(ballot(val > L) & OL & ~selfL) + __builtin_popcountll(ballot(val > R) & OR & ~selfR) +
-                      (sgt64(val, rootv) ? 1 : 0);
-        if (h > 0) {
-            const uint64_t fL = bperm64_addr(L, pc.addrF), fR = bperm64_addr(R, pc.addrF);
-            const int32_t fLI = bperm32_addr(IL, pc.addrF), fRI = bperm32_addr(IR, pc.addrF);
-            const bool odd = in_mask(0xAAAAAAAAAAAAAAAAull); // father slot p odd: an L half
-            const uint64_t f = odd ? fL : fR;
-            const int32_t fI = odd ? fLI : fRI;
-            const uint64_t mlt = ~0ull << ((1u << (B - h - 1)) - 1u); // chain index < h: bl > B - h
-            const bool wl = in_mask(OL & mlt), wr = in_mask(OR & mlt);
-            L = wl ? f : L;
-            IL = wl ? fI : IL;
-            R = wr ? f : R;
-            IR = wr ? fI : IR;
-            if (h == B - 1) { // val becomes the root; the old root moves to its child on the chain (lane 0)
-                const bool rl = in_mask(OL & 1ull), rr = in_mask(OR & 1ull);
-                L = rl ? rootv : L;
-                IL = rl ? rootI : IL;
-                R = rr ? rootv : R;
-                IR = rr ? rootI : IR;
-                rootI = valI;
-                const bool s63 = in_mask(1ull << 63);
-                R = s63 ? val : R;
-                IR = s63 ? valI : IR;
-                return val;
-            }
-        }
-        const uint32_t x = (s1 >> h) - 1u; // the slot of chain index h (>= 1 here)
-        const bool xs = in_mask(1ull << ((x - 1u) >> 1));
-        if (x & 1u) {
-            L = xs ? val : L;
-            IL = xs ? valI : IL;
-        } else {
-            R = xs ? val : R;
-            IR = xs ? valI : IR;
-        }
-        return rootv;
+        const uint64_t fL = bperm64_addr(L, pc.addrF), fR = bperm64_addr(R, pc.addrF);
+        const int32_t fIL = bperm32_addr(IL, pc.addrF), fIR = bperm32_addr(IR, pc.addrF);
+        const uint32_t B = (uint32_t)bitlen(k);
+        const bool s63 = in_mask(1ull << 63);
+        // m < 0 (x deeper than k) wraps to a shift of 57..63: the 64-bit shift gives 0, never a position
+        const uint32_t m = B - pc.bl;
+        const uint32_t t = (uint32_t)((uint64_t)k >> (m & 63u));
+        const uint32_t ciL = t == pc.xL ? m : 99u;
+        const uint32_t ciR = s63 ? B - 1u : (t == pc.xL + 1u ? m : 99u);
+        // the ancestors (index >= 1; index 0 is the new slot itself)
+        const uint64_t cL = (ciL - 1u) < 7u ? L : ~0ull, cR = (ciR - 1u) < 7u ? R : ~0ull;
+        const uint32_t h = (uint32_t)(__builtin_popcountll(ballot(val > cL)) + __builtin_popcountll(ballot(val > cR)));
+        const bool odd = in_mask(0xAAAAAAAAAAAAAAAAull); // father slot p odd: an L half
+        const uint64_t f = odd ? fL : fR;
+        const int32_t fI = odd ? fIL : fIR;
+        const bool wl = ciL < h, wr = ciR < h, xl = ciL == h, xr = ciR == h;
+        L = wl ? f : L;
+        IL = wl ? fI : IL;
+        L = xl ? val : L;
+        IL = xl ? valI : IL;
+        R = wr ? f : R;
+        IR = wr ? fI : IR;
+        R = xr ? val : R;
+        IR = xr ? valI : IR;
     }
 };
 
@@ -616,7 +605,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     uint64_t *lg = a.log + (size_t)blockIdx.x * (size_t)a.log_cap;
     const int ef = FIX128 ? 128 : a.ef, k = (FIX128 && LOGRES) ? 128 : a.k, deg0 = a.deg0;
     const int ef_search = FIX128 ? 128 : a.efSearch;
-    const int hop_bound = a.ntotal < (int64_t)INT32_MAX ? (int)a.ntotal : INT32_MAX;
+    const int hop_bound = a.hop_bound < (int64_t)INT32_MAX ? (int)a.hop_bound : INT32_MAX;
+    int64_t taken = 0;
     const PathConst pconst(lane);
     const uint32_t kInfKey = ord32(INFINITY);
 
@@ -625,6 +615,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         DRM_DBG(16u, q, 0, (uint32_t)a.n, 0u, 0u, 0u, 0u);
         if ((int64_t)q >= a.n)
             break;
+        if (++taken > a.item_bound) { // more items than the queue holds: a broken work-queue fetch
+            if (lane == 0)
+                atomicAdd(a.errors, 1u);
+            break;
+        }
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < k; j += 64) {
                 a.D[(int64_t)q * k + j] = INFINITY;
@@ -665,7 +660,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         hp.IL = -1;
         hp.IR = lane == 63 ? nearest : -1;
         int kc = 1;
-        uint64_t root = pack(dn, nearest); // slot 0
+        // the root's key (high word) and node id, current whenever the heap is full (kc == ef): the fill does not track
+        // them, they are read from lane 63's R once the heap is full, and after every full-heap replace
+        uint32_t rootHi = dn;
         int32_t rootI = nearest;
         // result set: the log (LOGRES) or a sorted register set of k <= 64 entries
         int logn = 0;
@@ -686,7 +683,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         // root, and only those at the root's distance can still be results: k of them, the smallest ids, are kept
         // (T = the root's key) -- then appends the staged entries
         auto log_compact = [&]() {
-            const uint32_t T = hi32(root);
+            const uint32_t T = rootHi;
             const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
             logn = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) {
                 __hip_atomic_store(lg + p, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -708,7 +705,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         };
         if (!LOGRES) {
             if (dn < thr)
-                add_result(root);
+                add_result(pack(dn, nearest));
         }
         int clear_n = 1;
         if (STATS && lane == 0) { // vt.set(entry)
@@ -765,9 +762,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const bool popR = lane == wl && pickR, popL = lane == wl && !pickR;
             hp.R = popR ? (hp.R & ~0xFFFFFFFFull) | kPopLo : hp.R;
             hp.L = popL ? (hp.L & ~0xFFFFFFFFull) | kPopLo : hp.L;
-            if (wl == 63 && (rightm >> 63))
-                root = (root & ~0xFFFFFFFFull) | kPopLo;
-            DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)__builtin_popcountll(validm), (uint32_t)kc, hi32(root));
+            DRM_DBG(2u, q, nstep, (uint32_t)v0, d0, (uint32_t)__builtin_popcountll(validm), (uint32_t)kc, rootHi);
             // count_below(d0): every slot in the heap (popped ones included); unused keys are ~0. The slot just popped
             // holds d0 itself, so at most ef - 1 slots lie below it: with efSearch >= ef (ef = max(efSearch, k), so
             // whenever k <= efSearch -- the pipeline's EF = K = 128) the check can never stop the search, and is skipped
@@ -868,9 +863,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // and is still there, or was rejected / evicted at a root that is now at or below its distance.
             uint64_t rem = actm;
             if (kc < ef) { // the heap fills: every link not in it is pushed
-                while (rem && kc < ef) {
+                while (rem) {
                     const int l = __builtin_ctzll(rem);
-                    rem &= rem - 1;
+                    asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
                     const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
                     const int32_t idl = __builtin_amdgcn_readlane(v1, l);
                     if (STAMPS)
@@ -882,16 +877,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     if (!LOGRES && key < thr)
                         add_result(val);
                     ++kc;
-                    if (ef == 128) {
-                        root = hp.push_fill(kc, val, idl, pconst, root, rootI);
-                    } else {
+                    if (ef == 128)
+                        hp.push_fill((uint32_t)kc, val, idl, pconst);
+                    else
                         hp.push(kc, val, idl, lane);
-                        root = readlane64(hp.R, 63);
-                        rootI = readlane32(hp.IR, 63);
+                    if (kc == ef) { // full: the root is read once, and kept current from here on
+                        rootHi = hp.root_hi();
+                        rootI = hp.root_id();
+                        break;
                     }
                 }
             }
-            rem &= ballot(dall < hi32(root)); // the heap is full here, or rem is empty
+            rem &= ballot(dall < rootHi); // the heap is full here, or rem is empty
             while (rem) { // MinimaxHeap::push on the full heap: pop the max, push val
                 const int l = __builtin_ctzll(rem);
                 asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
@@ -905,23 +902,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, 0u, (uint32_t)sn);
                 if (!LOGRES && key < thr)
                     add_result(val);
-                const uint32_t evk = hi32(root); // the evicted slot: the root (its node id in rootI)
+                const uint32_t evk = rootHi; // the evicted slot: the root (its node id in rootI)
                 const int32_t evi = rootI;
                 if (ef == 128) {
-                    root = hp.replace128(val, idl, pconst, lane, rootI);
+                    hp.replace128(val, idl, pconst, lane);
                     if (STAMPS)
                         st_acc[11] += 1u;
                 } else {
                     hp.pop(kc, lane);
                     hp.push(kc, val, idl, lane);
-                    root = readlane64(hp.R, 63);
-                    rootI = readlane32(hp.IR, 63);
                 }
+                rootHi = hp.root_hi();
+                rootI = hp.root_id();
                 // the root fell: links at or above it leave the candidate mask (one compare for the rest of the row)
-                rem &= ballot(dall < hi32(root));
+                rem &= ballot(dall < rootHi);
                 // LOGRES: an evicted result at the new root's distance can still be among the k results (the result
                 // handler breaks distance ties by node id, the MinimaxHeap by slot); any other evicted one cannot
-                if (LOGRES && evk == hi32(root)) {
+                if (LOGRES && evk == rootHi) {
                     if (sn == 64)
                         log_flush();
                     const bool at = lane == sn; // lane sn takes the entry (one compare, two selects)
@@ -965,7 +962,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             __builtin_amdgcn_s_waitcnt(0); // this wave's log stores have landed
             DRM_DBG(8u, q, nstep, 0u, 0u, 0u, 0u, 0u);
             __syncthreads();
-            const uint32_t T = kc == ef ? hi32(root) : 0xFFFFFFFFu;
+            const uint32_t T = kc == ef ? rootHi : 0xFFFFFFFFu;
             const uint32_t idthr = log_id_threshold(lg, logn, T, k, lane);
             DRM_DBG(9u, q, nstep, T, idthr, 0u, 0u, 0u);
             const int c = log_select(lg, logn, T, idthr, [&](int p, uint64_t e) { stage[p] = e; }, lane);
@@ -1003,14 +1000,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             a.D[o] = valid ? unord32(hi32(rv)) : INFINITY;
             a.I[o] = valid ? (int64_t)unpack_id(rv) : (int64_t)-1;
         }
-        DRM_DBG(5u, q, nstep, (uint32_t)logn, (uint32_t)overrun, (uint32_t)kc, hi32(root), 0u);
+        DRM_DBG(5u, q, nstep, (uint32_t)logn, (uint32_t)overrun, (uint32_t)kc, rootHi, 0u);
         if (lane == 0) {
             a.ndis[q] = overrun ? -1 : ndis + ndis0;
             a.nhops[q] = overrun ? -1 : nhops + nstep;
             if (a.nhops_upper)
                 a.nhops_upper[q] = nhops_upper;
             if (overrun)
-                atomicAdd(a.counter + 3, 1u);
+                atomicAdd(a.errors, 1u);
         }
         DRM_DBG(18u, q, nstep, 0u, 0u, 0u, 0u, 0u);
         if (STATS) { // VisitedTable::advance: clear exactly the bits this query set; they land before the next query
@@ -1063,7 +1060,7 @@ __global__ __launch_bounds__(256) void build_upper_codes_kernel(const int32_t *u
 
 void build_inline_rows(DeviceIndex &ix)
 {
-    if (ix.pq_M != 8 || ix.pq_nbits != 8 || ix.code_size != 8 || ix.deg0 > 64 || ix.deg0 < 1 || ix.vmode != 0 ||
+    if (ix.pq_M != 8 || ix.pq_nbits != 8 || ix.code_size != 8 || ix.deg0 > 64 || ix.deg0 < 1 ||
         ix.ntotal <= 0)
         return;
     const int64_t words = ((int64_t)ix.deg0 * 3 + 31) / 32 * 32; // deg0 x (id, 2 code words), 128-B rows
@@ -1095,7 +1092,7 @@ void build_inline_rows(DeviceIndex &ix)
 bool hnsw_pq_fast_supported(const DeviceIndex &ix, int k, int efc)
 {
     return ix.rows != nullptr && ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8 && ix.deg0 <= 64 &&
-           efc <= 128 && (k == efc || k <= 64) && ix.vmode == 0;
+           efc <= 128 && (k == efc || k <= 64);
 }
 
 void launch_hnsw_pq_fast(const SearchArgs &a, int slots, bool stamps, hipStream_t stream)

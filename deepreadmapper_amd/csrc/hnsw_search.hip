@@ -375,13 +375,10 @@ struct PairHeap {
     }
 };
 
-constexpr int kHashSlots = 2048; // LDS visited hash per wave (8 KB)
 
-__device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - 11); }
-
-// VMODE 0: visited = per-slot HBM bitmap (atomicOr test-and-set).
-// VMODE 1: visited = LDS open-addressing hash; when it nears capacity the query spills it into the
-//          HBM bitmap and continues there (exact in both regimes).
+// The visited set is a per-slot HBM bitmap (atomicOr test-and-set), cleared from a list after each query.
+// Bounded: a query past a.hop_bound level-0 hops, or a wave past a.item_bound work items, ends with an error count
+// (a.errors; drm_search returns DRM_ERR_INTERNAL) instead of looping.
 // STAMPS (diagnostic builds only): per-section s_memtime sums -> a.stamps[section], for time shares.
 #define DRM_STAMP(idx)                                                                                      \
     do {                                                                                                    \
@@ -394,7 +391,7 @@ __device__ __forceinline__ uint32_t vhash(int32_t v) { return ((uint32_t)v * 0x9
         }                                                                                                   \
     } while (0)
 
-template <int R, bool FAST8, int VMODE, bool SPEC, bool STAMPS = false>
+template <int R, bool FAST8, bool STAMPS = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hnsw_pq_search_kernel(SearchArgs a)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -402,19 +399,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
-    int32_t *ht = reinterpret_cast<int32_t *>(lut + a.M * a.ksub); // visited hash (VMODE 1)
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
     const uint32_t kInfKey = ord32(INFINITY);
-    // queue: 0..n-1, or (fallback pass) the *qcount query ids in qlist
-    const int64_t nq = a.qlist ? (int64_t)*a.qcount : a.n;
-
+    int64_t taken = 0;
     for (;;) {
-        int q = wave_next_item(a.counter, lane);
-        if ((int64_t)q >= nq)
+        const int q = wave_next_item(a.counter, lane);
+        if ((int64_t)q >= a.n)
             break;
-        if (a.qlist)
-            q = __builtin_amdgcn_readfirstlane(a.qlist[q]);
+        if (++taken > a.item_bound) { // more items than the queue holds: a broken work-queue fetch
+            if (lane == 0)
+                atomicAdd(a.errors, 1u);
+            break;
+        }
 
         if (a.entry_point < 0 || a.ntotal == 0) {
             for (int j = lane; j < a.k; j += 64) {
@@ -431,11 +428,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         }
         DRM_STAMP(7);
         // --- set_query
-        if (VMODE == 1) {
-            int4 *h4 = reinterpret_cast<int4 *>(ht);
-            for (int t = lane; t < kHashSlots / 4; t += 64)
-                h4[t] = make_int4(-1, -1, -1, -1);
-        }
         build_lut(a, q, lut, lane);
         DRM_STAMP(0);
         int32_t nearest;
@@ -499,25 +491,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             wr(ci, 0, (uint32_t)nearest);
         }
         add_result(dn, nearest);
-        int clear_n = 0, hcount = 0;
-        bool spilled = (VMODE == 0);
-        if (VMODE == 1) {
-            if (lane == 0)
-                ht[vhash(nearest)] = nearest;
-            hcount = 1;
-        } else {
-            if (lane == 0) {
-                vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
-                if (a.clear_cap > 0)
-                    clr[0] = nearest;
-            }
-            clear_n = 1;
+        int clear_n = 1;
+        if (lane == 0) {
+            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
+            if (a.clear_cap > 0)
+                clr[0] = nearest;
         }
         __syncthreads();
 
         int nstep = 0, ndis0 = 0;
+        bool overrun = false;
         int32_t pred = -1, v1_pref = -1; // row of the node predicted to be popped next, loaded early
         while (nvalid > 0) {
+            if (nstep > a.hop_bound) { // a node is expanded at most once: past the bound the bookkeeping is broken
+                overrun = true;
+                break;
+            }
             // pop_min: smallest distance among valid slots, ties -> highest slot
             uint32_t bh = 0xFFFFFFFFu, bl = 0xFFFFFFFFu;
             const int sL = 2 * lane + 1, sR = (lane == 63) ? 0 : 2 * lane + 2; // PAIR slots of this lane
@@ -581,43 +570,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             const int jmax = negm ? (__ffsll((unsigned long long)negm) - 1) : a.deg0;
             const bool act = lane < jmax;
             uint2 c8 = make_uint2(0u, 0u);
-            if (SPEC && FAST8 && act)
+            if (FAST8 && act)
                 c8 = load_code8<FAST8>(a, v1); // issued before the visited test: overlaps its latency
-            if (VMODE == 1 && !spilled && hcount + jmax > (kHashSlots * 7) / 8) {
-                // spill the LDS set into the HBM bitmap + clear list, continue there
-                for (int t = lane; t < kHashSlots; t += 64) {
-                    const int32_t hv = ht[t];
-                    const bool has = hv >= 0;
-                    const uint64_t m = __ballot(has);
-                    if (has) {
-                        vis_test_set(&vis[hv >> 5], 1u << (hv & 31));
-                        const int p = clear_n + __popcll(m & lanes_below(lane));
-                        if (p < a.clear_cap)
-                            clr[p] = hv;
-                    }
-                    clear_n += __popcll(m);
-                }
-                spilled = true;
-            }
             bool fresh = false;
             if (act) {
-                if (VMODE == 1 && !spilled) {
-                    uint32_t h = vhash(v1);
-                    for (;;) {
-                        const int32_t old = atomicCAS(&ht[h], -1, v1);
-                        if (old == -1) {
-                            fresh = true;
-                            break;
-                        }
-                        if (old == v1)
-                            break;
-                        h = (h + 1) & (kHashSlots - 1);
-                    }
-                } else {
-                    const uint32_t bit = 1u << (v1 & 31);
-                    const uint32_t old = vis_test_set(&vis[v1 >> 5], bit);
-                    fresh = (old & bit) == 0u;
-                }
+                const uint32_t bit = 1u << (v1 & 31);
+                const uint32_t old = vis_test_set(&vis[v1 >> 5], bit);
+                fresh = (old & bit) == 0u;
             }
             if (a.check_dups) { // a repeated id in one row: only its first occurrence is fresh
                 for (int j = 0; j < jmax; ++j) {
@@ -630,13 +589,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             const uint64_t fm = __ballot(fresh);
             const int nf = __popcll(fm);
             const int clear_base = clear_n;
-            if (spilled)
-                clear_n += nf;
-            else
-                hcount += nf;
+            clear_n += nf;
             uint32_t dk = 0;
             if (fresh) {
-                if (!(SPEC && FAST8))
+                if (!FAST8)
                     c8 = load_code8<FAST8>(a, v1);
                 dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
             }
@@ -675,7 +631,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
                 }
             }
             // clear-list entries are stored after the loads above so that no wait covers them
-            if (spilled && fresh) {
+            if (fresh) {
                 const int p = clear_base + __popcll(fm & lanes_below(lane));
                 if (p < a.clear_cap)
                     clr[p] = v1;
@@ -733,259 +689,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             }
         }
         if (lane == 0) {
-            a.ndis[q] = ndis + ndis0;
-            a.nhops[q] = nhops + nstep;
+            a.ndis[q] = overrun ? -1 : ndis + ndis0;
+            a.nhops[q] = overrun ? -1 : nhops + nstep;
             if (a.nhops_upper)
                 a.nhops_upper[q] = nhops_upper;
+            if (overrun)
+                atomicAdd(a.errors, 1u);
         }
 
         // --- VisitedTable::advance: clear exactly the HBM bits this query set
-        if (spilled) {
-            if (clear_n <= a.clear_cap) {
-                for (int t = lane; t < clear_n; t += 64)
-                    vis[clr[t] >> 5] = 0u;
-            } else {
-                for (int64_t w = lane; w < a.vis_words; w += 64)
-                    vis[w] = 0u;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        DRM_STAMP(6);
-    }
-    if (STAMPS && lane_id() == 0 && a.stamps)
-        for (int i = 0; i < 12; ++i)
-            atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
-}
-
-
-// ------------------------------------------------------------------------------------------------
-// Fast path: the MinimaxHeap and the result heap as ONE register-resident array sorted by key.
-//
-// While no two entries of the candidate set share a distance, faiss's behaviour does not depend on
-// the heap's slot layout: pop_min's minimum is unique, the evicted maximum is unique, count_below(d0)
-// is the popped entry's rank, and (k <= ef, same acceptance rule `d < max`) the result heap holds
-// exactly the first k entries of the candidate set. So slot s (lane s & 63, register s >> 6) keeps
-// the s-th smallest (key, id), bit 31 of the id marks a popped entry, pushing is one sorted insert
-// (ballot rank + DPP shift), pop_min is the first unpopped slot and eviction drops the last slot.
-// A query that would insert a distance already present (or +inf) is abandoned and appended to
-// a.fb_list; the exact kernel above re-runs it, so every output is bit-identical to the oracle.
-template <int R, bool FAST8, bool STAMPS = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hnsw_pq_search_sorted_kernel(
-    SearchArgs a)
-{
-    extern __shared__ __align__(16) unsigned char smem[];
-    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    const int lane = lane_id();
-    float *lut = reinterpret_cast<float *>(smem);
-    uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
-    int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
-    const uint32_t kInfKey = ord32(INFINITY);
-    constexpr uint32_t kPopped = 0x80000000u;
-
-    for (;;) {
-        const int q = wave_next_item(a.counter, lane);
-        if ((int64_t)q >= a.n)
-            break;
-
-        if (a.entry_point < 0 || a.ntotal == 0) {
-            for (int j = lane; j < a.k; j += 64) {
-                a.D[(int64_t)q * a.k + j] = INFINITY;
-                a.I[(int64_t)q * a.k + j] = -1;
-            }
-            if (lane == 0) {
-                a.ndis[q] = 0;
-                a.nhops[q] = 0;
-                if (a.nhops_upper)
-                    a.nhops_upper[q] = 0;
-            }
-            continue;
-        }
-        DRM_STAMP(7);
-        build_lut(a, q, lut, lane);
-        DRM_STAMP(0);
-        int32_t nearest;
-        uint32_t dn;
-        int ndis, nhops;
-        greedy_upper<FAST8>(a, lut, lane, nearest, dn, ndis, nhops);
-        const int nhops_upper = nhops;
-        DRM_STAMP(1);
-
-        // candidate set: unused slots hold (~0, ~0) -- above every key, and "popped"
-        uint32_t ck[R], ci[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            ck[r] = 0xFFFFFFFFu;
-            ci[r] = 0xFFFFFFFFu;
-        }
-        wr(ck, 0, dn);
-        wr(ci, 0, (uint32_t)nearest);
-        int kc = 1, nvalid = 1;
-        bool tie = dn == kInfKey; // the result handler would reject +inf, the candidate heap not
-        if (lane == 0) {
-            vis_test_set(&vis[nearest >> 5], 1u << (nearest & 31));
-            if (a.clear_cap > 0)
-                clr[0] = nearest;
-        }
-        int clear_n = 1;
-
-        int nstep = 0, ndis0 = 0;
-        int32_t pred = -1, v1_pref = -1;
-        while (nvalid > 0 && !tie) {
-            // pop_min = first unpopped slot; count_below(d0) = its rank
-            int imin = 64 * R;
-#pragma unroll
-            for (int r = R - 1; r >= 0; --r) {
-                const uint64_t m = __ballot((ci[r] & kPopped) == 0u);
-                if (m)
-                    imin = 64 * r + __builtin_ctzll(m);
-            }
-            const int32_t v0 = (int32_t)rd(ci, imin);
-            wr(ci, imin, (uint32_t)v0 | kPopped);
-            nvalid--;
-            if (imin >= a.efSearch)
-                break;
-
-            DRM_STAMP(2);
-            int32_t v1 = v1_pref;
-            if (v0 != pred)
-                v1 = (lane < a.deg0) ? a.nbr0[(size_t)v0 * (size_t)a.deg0 + lane] : -1;
-            const uint64_t negm = __ballot(lane < a.deg0 && v1 < 0);
-            const int jmax = negm ? (__ffsll((unsigned long long)negm) - 1) : a.deg0;
-            const bool act = lane < jmax;
-            uint2 c8 = make_uint2(0u, 0u);
-            if (FAST8 && act)
-                c8 = load_code8<FAST8>(a, v1);
-            bool fresh = false;
-            if (act) {
-                const uint32_t bit = 1u << (v1 & 31);
-                const uint32_t old = vis_test_set(&vis[v1 >> 5], bit);
-                fresh = (old & bit) == 0u;
-            }
-            if (a.check_dups) {
-                for (int j = 0; j < jmax; ++j) {
-                    const int32_t vj = __shfl(v1, j, 64);
-                    if (j < lane && vj == v1)
-                        fresh = false;
-                }
-            }
-            DRM_STAMP(3);
-            const uint64_t fm = __ballot(fresh);
-            const int nf = __popcll(fm);
-            const int clear_base = clear_n;
-            clear_n += nf;
-            uint32_t dk = 0xFFFFFFFFu;
-            if (fresh) {
-                if (!FAST8)
-                    c8 = load_code8<FAST8>(a, v1);
-                dk = ord32(pq_distance_code<FAST8>(a, lut, v1, c8));
-            }
-            ndis0 += nf;
-            {
-                // prefetch the row of the likely next pop_min (a wrong guess only costs a reload)
-                int inext = 64 * R;
-#pragma unroll
-                for (int r = R - 1; r >= 0; --r) {
-                    const uint64_t m = __ballot((ci[r] & kPopped) == 0u);
-                    if (m)
-                        inext = 64 * r + __builtin_ctzll(m);
-                }
-                const uint32_t hk = inext < 64 * R ? rd(ck, inext) : 0xFFFFFFFFu;
-                const uint32_t fmin = wave_min_u32(dk);
-                pred = -1;
-                if (fmin < hk)
-                    pred = __builtin_amdgcn_readlane(v1, __builtin_ctzll(__ballot(dk == fmin)));
-                else if (hk != 0xFFFFFFFFu)
-                    pred = (int32_t)(rd(ci, inext) & ~kPopped);
-                if (pred >= 0)
-                    v1_pref = (lane < a.deg0) ? a.nbr0[(size_t)pred * (size_t)a.deg0 + lane] : -1;
-            }
-            if (fresh) {
-                const int p = clear_base + __popcll(fm & lanes_below(lane));
-                if (p < a.clear_cap)
-                    clr[p] = v1;
-            }
-            DRM_STAMP(4);
-            // push each fresh link in row order
-            uint64_t rem = fm;
-            while (rem) {
-                const int l = __builtin_ctzll(rem);
-                rem &= rem - 1;
-                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dk, l);
-                const int32_t id = __builtin_amdgcn_readlane(v1, l);
-                const bool full = kc == a.ef;
-                if (full && key >= rd(ck, kc - 1))
-                    continue; // MinimaxHeap::push rejects; the result handler rejects too (k <= ef)
-                int pos = 0;
-                uint64_t eq = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    pos += __popcll(__ballot(ck[r] < key));
-                    eq |= __ballot(ck[r] == key);
-                }
-                if (eq != 0 || key == kInfKey) {
-                    tie = true;
-                    break;
-                }
-                if (full) { // drop the maximum (slot ef-1)
-                    if ((rd(ci, kc - 1) & kPopped) == 0u)
-                        nvalid--;
-                    kc--;
-                }
-                uint32_t pk[R], pi[R];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t carry_k = r ? (uint32_t)__builtin_amdgcn_readlane((int)ck[r - 1], 63) : 0u;
-                    const uint32_t carry_i = r ? (uint32_t)__builtin_amdgcn_readlane((int)ci[r - 1], 63) : 0u;
-                    pk[r] = wave_shr1(carry_k, ck[r]);
-                    pi[r] = wave_shr1(carry_i, ci[r]);
-                }
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int s2 = lane + 64 * r;
-                    if (s2 > pos) {
-                        ck[r] = pk[r];
-                        ci[r] = pi[r];
-                    } else if (s2 == pos) {
-                        ck[r] = key;
-                        ci[r] = (uint32_t)id;
-                    }
-                }
-                kc++;
-                nvalid++;
-                if (full && kc < 64 * R) { // the dropped maximum was shifted into slot ef
-                    wr(ck, kc, 0xFFFFFFFFu);
-                    wr(ci, kc, 0xFFFFFFFFu);
-                }
-            }
-            nstep++;
-            DRM_STAMP(5);
-        }
-
-        DRM_STAMP(2);
-        if (tie) { // hand the query to the exact kernel
-            if (lane == 0)
-                a.fb_list[atomicAdd(a.fb_count, 1u)] = q;
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int j = lane + 64 * r;
-                if (j < a.k) {
-                    const int64_t o = (int64_t)q * a.k + j;
-                    const bool valid = j < kc;
-                    a.D[o] = valid ? unord32(ck[r]) : INFINITY;
-                    a.I[o] = valid ? (int64_t)(int32_t)(ci[r] & ~kPopped) : (int64_t)-1;
-                }
-            }
-            if (lane == 0) {
-                a.ndis[q] = ndis + ndis0;
-                a.nhops[q] = nhops + nstep;
-                if (a.nhops_upper)
-                    a.nhops_upper[q] = nhops_upper;
-            }
-        }
-        // VisitedTable::advance
         if (clear_n <= a.clear_cap) {
             for (int t = lane; t < clear_n; t += 64)
                 vis[clr[t] >> 5] = 0u;
@@ -1001,6 +713,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
         for (int i = 0; i < 12; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
+
 
 } // namespace
 
@@ -1038,15 +751,21 @@ void reserve_search_scratch(DeviceIndex &ix)
     ix.device_bytes += (int64_t)sizeof(uint64_t) * slots * cap;
 }
 
-void check_search_errors(const DeviceIndex &ix)
+void check_search_errors(DeviceIndex &ix)
 {
     if (!ix.counter)
         return;
     uint32_t c[4] = {0, 0, 0, 0};
     DRM_HIP_CHECK(hipMemcpy(c, ix.counter, sizeof(c), hipMemcpyDeviceToHost));
-    if (c[3])
-        throw Error(DRM_ERR_INTERNAL, std::to_string(c[3]) + " queries exceeded the search's hop bound (ntotal hops)");
+    if (c[3]) {
+        DRM_HIP_CHECK(hipMemset(ix.counter + 3, 0, sizeof(uint32_t))); // reported once
+        throw Error(DRM_ERR_INTERNAL, std::to_string(c[3]) + " queries exceeded the search's hop bound or waves their "
+                                                             "work-item bound (DESIGN.md sec. 4.1): search state broken");
+    }
 }
+
+int64_t search_hop_bound(const DeviceIndex &ix) { return ix.hop_bound > 0 ? std::min(ix.hop_bound, ix.ntotal) : ix.ntotal; }
+int64_t search_item_bound(const DeviceIndex &ix, int64_t n) { return ix.item_bound > 0 ? std::min(ix.item_bound, n) : n; }
 
 void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int ef, float *d_D, int64_t *d_I,
                         int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, hipStream_t stream)
@@ -1074,9 +793,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
         launch_hnsw_search_lds(ix, d_x, n, k, ef, d_D, d_I, d_ndis, d_nhops, d_nhops_upper, stream);
         return;
     }
-    const int vmode = ix.vmode;
-    const size_t scratch = vmode == 1 ? sizeof(int32_t) * 2048 : 0;
-    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub + scratch; // LUT, [hash]
+    const size_t lds = sizeof(float) * (size_t)ix.pq_M * ix.ksub; // the LUT
     if (lds > 160 * 1024)
         throw Error(DRM_ERR_UNSUPPORTED, "search workspace does not fit in LDS");
 
@@ -1085,7 +802,7 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     int per_cu = std::max(1, std::min(ix.waves_per_cu, (int)((160 * 1024) / lds)));
     int slots = (int)std::min<int64_t>(n, (int64_t)cus * per_cu);
     // (re)allocate per-slot workspace: the lean kernel needs the bitmap only to count faiss's ndis
-    const bool fast_path = ix.use_fast && !ix.try_sorted && hnsw_pq_fast_supported(ix, k, efc);
+    const bool fast_path = ix.use_fast && hnsw_pq_fast_supported(ix, k, efc);
     const bool need_bitmap = !fast_path || ix.exact_stats;
     const int64_t words = (ix.ntotal + 31) / 32;
     if (need_bitmap && (slots > ix.n_slots || words != ix.vis_words)) {
@@ -1152,6 +869,9 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
     a.clear_list = ix.clear_list;
     a.clear_cap = ix.clear_cap;
     a.counter = ix.counter;
+    a.errors = ix.counter + 3;
+    a.hop_bound = search_hop_bound(ix);
+    a.item_bound = search_item_bound(ix, n);
     a.check_dups = ix.has_dup_links;
     a.stamps = ix.stamps;
     a.trace = ix.trace;
@@ -1184,53 +904,22 @@ void launch_hnsw_search(DeviceIndex &ix, const float *d_x, int64_t n, int k, int
         launch_hnsw_pq_fast(a, slots, ix.stamps != nullptr, stream);
         return;
     }
-    // The sorted-array pass only pays off when distance ties are rare; stride-1 genome windows
-    // share PQ codes so often that nearly every query falls back. Opt-in via DRM_SEARCH_SORTED=1.
-    const bool sorted_path = ix.try_sorted && !ix.force_exact && vmode == 0 && R <= 2;
     DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 4 * sizeof(uint32_t), stream));
-#define DRM_LAUNCH_EXACT(RR, F8, VM)                                                                           \
-    hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8, VM, F8>), dim3(slots), dim3(64), lds, stream, a)
-#define DRM_LAUNCH_EXACT_R(F8, VM)                                                                             \
+#define DRM_LAUNCH_EXACT(RR, F8)                                                                               \
+    hipLaunchKernelGGL((hnsw_pq_search_kernel<RR, F8>), dim3(slots), dim3(64), lds, stream, a)
+#define DRM_LAUNCH_EXACT_R(F8)                                                                                 \
     switch (R) {                                                                                                \
-    case 1: DRM_LAUNCH_EXACT(1, F8, VM); break;                                                                 \
-    case 2: DRM_LAUNCH_EXACT(2, F8, VM); break;                                                                 \
-    case 3: case 4: DRM_LAUNCH_EXACT(4, F8, VM); break;                                                         \
-    default: DRM_LAUNCH_EXACT(8, F8, VM); break;                                                                \
+    case 1: DRM_LAUNCH_EXACT(1, F8); break;                                                                     \
+    case 2: DRM_LAUNCH_EXACT(2, F8); break;                                                                     \
+    case 3: case 4: DRM_LAUNCH_EXACT(4, F8); break;                                                             \
+    default: DRM_LAUNCH_EXACT(8, F8); break;                                                                    \
     }
-    if (sorted_path) {
-        // pass 1: sorted-array kernel; queries that meet a distance tie go to fb_list
-        if (n > ix.fb_cap) {
-            if (ix.fb_list)
-                DRM_HIP_CHECK(hipFree(ix.fb_list));
-            ix.fb_list = nullptr;
-            DRM_HIP_CHECK(hipMalloc(&ix.fb_list, sizeof(int32_t) * (size_t)n));
-            ix.fb_cap = n;
-        }
-        a.fb_list = ix.fb_list;
-        a.fb_count = ix.counter + 1;
-        if (fast8 && ix.stamps && R == 2)
-            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, true, true>), dim3(slots), dim3(64), lds, stream, a);
-        else if (fast8 && R == 2)
-            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, true>), dim3(slots), dim3(64), lds, stream, a);
-        else if (fast8)
-            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<1, true>), dim3(slots), dim3(64), lds, stream, a);
-        else if (R == 2)
-            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<2, false>), dim3(slots), dim3(64), lds, stream, a);
-        else
-            hipLaunchKernelGGL((hnsw_pq_search_sorted_kernel<1, false>), dim3(slots), dim3(64), lds, stream, a);
-        DRM_HIP_CHECK(hipGetLastError());
-        // pass 2: the exact kernel over fb_list (its waves exit at once when the list is empty)
-        a.qlist = ix.fb_list;
-        a.qcount = ix.counter + 1;
-        a.counter = ix.counter + 2;
-        a.stamps = nullptr;
-        if (fast8) { DRM_LAUNCH_EXACT_R(true, 0) } else { DRM_LAUNCH_EXACT_R(false, 0) }
-    } else if (fast8 && ix.stamps && R == 2 && vmode == 0) {
-        hipLaunchKernelGGL((hnsw_pq_search_kernel<2, true, 0, true, true>), dim3(slots), dim3(64), lds, stream, a);
+    if (fast8 && ix.stamps && R == 2) {
+        hipLaunchKernelGGL((hnsw_pq_search_kernel<2, true, true>), dim3(slots), dim3(64), lds, stream, a);
     } else if (fast8) {
-        if (vmode == 1) { DRM_LAUNCH_EXACT_R(true, 1) } else { DRM_LAUNCH_EXACT_R(true, 0) }
+        DRM_LAUNCH_EXACT_R(true)
     } else {
-        if (vmode == 1) { DRM_LAUNCH_EXACT_R(false, 1) } else { DRM_LAUNCH_EXACT_R(false, 0) }
+        DRM_LAUNCH_EXACT_R(false)
     }
 #undef DRM_LAUNCH_EXACT_R
 #undef DRM_LAUNCH_EXACT

@@ -186,10 +186,16 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_lds_kernel(SearchArgs a)
     uint32_t *vis = a.visited + (size_t)blockIdx.x * (size_t)a.vis_words;
     int32_t *clr = a.clear_list + (size_t)blockIdx.x * (size_t)a.clear_cap;
 
+    int64_t taken = 0;
     for (;;) {
         const int64_t q = wave_next_item(a.counter, lane);
         if (q >= a.n)
             break;
+        if (++taken > a.item_bound) { // more items than the queue holds: a broken work-queue fetch
+            if (lane == 0)
+                atomicAdd(a.errors, 1u);
+            break;
+        }
 
         int32_t ndis = 0, nhops = 0;
         // --- HeapBlockResultHandler::begin: heapify k x (+inf, -1)
@@ -280,7 +286,12 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_lds_kernel(SearchArgs a)
         __syncthreads();
 
         int nstep = 0, ndis0 = 0;
+        bool overrun = false;
         while (nvalid > 0) {
+            if (nstep > a.hop_bound) { // a node is expanded at most once: past the bound the bookkeeping is broken
+                overrun = true;
+                break;
+            }
             // pop_min: min distance over valid slots, ties -> highest slot
             uint64_t best = ~0ull;
             for (int s = lane; s < kc; s += 64) {
@@ -402,10 +413,12 @@ __global__ __launch_bounds__(64) void hnsw_pq_search_lds_kernel(SearchArgs a)
             }
         }
         if (lane == 0) {
-            a.ndis[q] = ndis + ndis0;
-            a.nhops[q] = nhops + nstep;
+            a.ndis[q] = overrun ? -1 : ndis + ndis0;
+            a.nhops[q] = overrun ? -1 : nhops + nstep;
             if (a.nhops_upper)
                 a.nhops_upper[q] = nhops;
+            if (overrun)
+                atomicAdd(a.errors, 1u);
         }
 
         // --- VisitedTable::advance: clear exactly the bits this query set
@@ -509,9 +522,12 @@ void launch_hnsw_search_lds(DeviceIndex &ix, const float *d_x, int64_t n, int k,
     a.clear_list = ix.clear_list;
     a.clear_cap = ix.clear_cap;
     a.counter = ix.counter;
+    a.errors = ix.counter + 3;
+    a.hop_bound = search_hop_bound(ix);
+    a.item_bound = search_item_bound(ix, n);
     a.check_dups = ix.has_dup_links;
 
-    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, sizeof(uint32_t), stream));
+    DRM_HIP_CHECK(hipMemsetAsync(ix.counter, 0, 4 * sizeof(uint32_t), stream)); // queue head and error count
     const bool fast8 = (ix.pq_M == 8 && ix.pq_nbits == 8 && ix.code_size == 8);
     if (fast8)
         hipLaunchKernelGGL(hnsw_pq_search_lds_kernel<true>, dim3(slots), dim3(64), lds, stream, a);

@@ -795,23 +795,14 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     a.cand_ids = refs.ws_ids;
     a.cand_scores = refs.ws_scores;
     a.ncand = refs.ws_ncand;
-    // One one-wave workgroup per query up to 65536 (grid-stride beyond). refs.sw_waves_per_cu > 0 caps the
-    // grid at that many resident waves per CU instead, leaving the rest of every CU to a search kernel
-    // running beside the rerank on another stream (drm_refs_set_sw_waves).
-    int64_t gcap = 65536;
-    if (refs.sw_waves_per_cu > 0) {
-        int cus = 0;
-        DRM_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, refs.device));
-        gcap = (int64_t)std::max(cus, 1) * refs.sw_waves_per_cu;
-    }
-    const int grid = (int)std::min<int64_t>(a.nq, gcap);
+    // the bit-profile kernel: one one-wave workgroup per query up to 65536 (grid-stride beyond)
+    const int grid = (int)std::min<int64_t>(a.nq, 65536);
 #ifndef DRM_SW_F16_GRID_CAP
 #define DRM_SW_F16_GRID_CAP (1 << 30)
 #endif
     // the pair-profile kernel: one workgroup per query (a query is ~270k issue cycles of one wave, so the grid's
     // tail is one query, not the 19-20 a 65536-wave grid-stride hands each wave at C5)
-    const int grid_f16 =
-        (int)std::min<int64_t>(a.nq, refs.sw_waves_per_cu > 0 ? gcap : (int64_t)DRM_SW_F16_GRID_CAP);
+    const int grid_f16 = (int)std::min<int64_t>(a.nq, (int64_t)DRM_SW_F16_GRID_CAP);
     const size_t cand_lds = sizeof(uint32_t) * (size_t)cmax; // sw_score_f16_kernel's candidate list
     // fp16 pair-profile kernel for queries up to 152 bytes; the bit-profile kernel re-scores the
     // queries it flagged, and takes longer queries (or everything when DRM_SW_BITPROFILE=1).

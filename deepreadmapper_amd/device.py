@@ -12,12 +12,44 @@ def device_count():
     return n.value
 
 
+class DeviceProps(C.Structure):
+    _fields_ = [("cu_count", C.c_int32), ("clock_khz", C.c_int32), ("total_mem", C.c_int64), ("lds_per_cu", C.c_int32),
+                ("arch", C.c_char * 64)]
+
+
+def device_props(dev=0):
+    """drm_device_get_props: CU count, peak engine clock (kHz), HBM bytes, LDS per CU, arch, read at run time."""
+    p = DeviceProps()
+    check(lib().drm_device_get_props(int(dev), C.byref(p)))
+    return {"cu_count": p.cu_count, "clock_hz": p.clock_khz * 1e3, "total_mem": p.total_mem,
+            "lds_per_cu": p.lds_per_cu, "arch": p.arch.decode()}
+
+
 def set_device(dev):
     check(lib().drm_set_device(int(dev)))
 
 
 def synchronize():
     check(lib().drm_device_sync())
+
+
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def host_checksum(a):
+    """The host form of drm_device_checksum over the bytes of array a: sum mod 2^64 over its 8-byte little-endian
+    words w_i (the last zero-padded) of splitmix64(w_i + i * 0x9E3779B97F4A7C15)."""
+    b = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+    pad = (-len(b)) % 8
+    if pad:
+        b = np.concatenate([b, np.zeros(pad, np.uint8)])
+    w = b.view("<u8")
+    with np.errstate(over="ignore"):
+        z = w + np.arange(len(w), dtype=np.uint64) * _GOLD
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int(z.sum(dtype=np.uint64))
 
 
 class DeviceBuffer:
@@ -52,6 +84,15 @@ class DeviceBuffer:
 
     def zero(self):
         check(lib().drm_memset(self.ptr, 0, max(self.nbytes, 1)))
+
+    def checksum(self, row_lo=0, row_hi=None, stream=None):
+        """drm_device_checksum of rows [row_lo, row_hi) (first axis); equals host_checksum of the same rows."""
+        row = self.nbytes // self.shape[0] if self.shape and self.shape[0] else 0
+        row_hi = self.shape[0] if row_hi is None else row_hi
+        out = C.c_uint64(0)
+        check(lib().drm_device_checksum(C.c_void_p(self.ptr + row_lo * row), C.c_int64((row_hi - row_lo) * row),
+                                        C.byref(out), stream.handle if stream is not None else None))
+        return int(out.value)
 
     def free(self):
         if self.ptr:

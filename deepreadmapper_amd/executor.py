@@ -86,8 +86,8 @@ def search_rerank(index, table, x, queries=None, k=128, ef=128, k_clusters=None,
 def search_rerank_device(index, table, d_x, n, d_queries, d_q_len, q_stride, d_D, d_I, d_sw_scores, d_sw_ids,
                          d_status, k=128, ef=128, k_clusters=None, stride=1, d_ndis=None, d_nhops=None,
                          d_nhops_upper=None, stream=None, stats=False):
-    """drm_search_rerank_device: search + SW rerank on DeviceBuffers, the search of batch b beside the rerank
-    of batch b-1 on the same CUs. stats=True synchronises and returns the PipelineStats."""
+    """drm_search_rerank_device: search, then SW rerank, on DeviceBuffers (the caller's stream). stats=True
+    synchronises and returns the PipelineStats."""
     kc = k if k_clusters is None else k_clusters
     st = PipelineStats() if stats else None
     p = lambda b: b.ptr if b is not None else None  # noqa: E731

@@ -56,10 +56,10 @@ class HnswFlatIndex:
         check(lib().drm_flat_search_overflows(self.handle, C.byref(c)))
         return int(c.value)
 
-    def fallbacks(self):
-        """Queries of the last search redone by the exact heap-replay pass (distance ties)."""
+    def search_errors(self):
+        """drm_flat_search_errors: queries past the hop bound / waves past the item bound (syncs, resets)."""
         c = C.c_int64(0)
-        check(lib().drm_flat_search_fallbacks(self.handle, C.byref(c)))
+        check(lib().drm_flat_search_errors(self.handle, C.byref(c)))
         return int(c.value)
 
     def free(self):

@@ -57,11 +57,12 @@ class HnswPqIndex:
         (the default) the lean kernel reports the distances it computed. Results do not depend on it."""
         check(lib().drm_index_set_exact_stats(self.handle, 1 if on else 0))
 
-    def fallbacks(self):
-        """Queries of the last search that met a distance tie and took the exact kernel (syncs)."""
+    def search_errors(self):
+        """drm_index_search_errors: queries past the hop bound / waves past the item bound since the last check
+        (syncs, resets the count); drm_search itself fails with DRM_ERR_INTERNAL when it is non-zero."""
         import ctypes as C
         c = C.c_int64(0)
-        check(lib().drm_search_fallbacks(self.handle, C.byref(c)))
+        check(lib().drm_index_search_errors(self.handle, C.byref(c)))
         return int(c.value)
 
     def free(self):

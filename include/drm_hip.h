@@ -62,11 +62,26 @@ const char *drm_last_error(void);
 int drm_version(void); /* major*10000 + minor*100 + patch */
 int drm_device_count(int *n);
 int drm_set_device(int device);
+/* The device's shape, read at run time (hipGetDeviceProperties): compute units, peak engine clock (kHz), HBM
+ * bytes, LDS bytes per CU, architecture name. bench.py prices its issue ceilings with these. */
+typedef struct {
+    int32_t cu_count;
+    int32_t clock_khz;
+    int64_t total_mem;
+    int32_t lds_per_cu;
+    char arch[64];
+} drm_device_props;
+int drm_device_get_props(int device, drm_device_props *out);
 int drm_device_sync(void);
 int drm_malloc(void **ptr, size_t bytes);
 int drm_free(void *ptr);
 int drm_memset(void *ptr, int value, size_t bytes);
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes);
+/* A 64-bit checksum of nbytes of device memory (8-byte aligned): the sum, mod 2^64, over the little-endian 8-byte
+ * words w_i (the last one zero-padded) of splitmix64(w_i + i * 0x9E3779B97F4A7C15). Position-dependent, so rows
+ * landing at the wrong offset change it; used to verify the RCCL result gather (bench.py) without copying the
+ * gathered rows to the host. Enqueued on `stream`, which it synchronises. No reference counterpart (a tool). */
+int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *stream);
 int drm_memcpy_d2h(void *dst, const void *src, size_t bytes);
 int drm_stream_create(void **stream);
 int drm_stream_destroy(void *stream);
@@ -108,18 +123,20 @@ int drm_search_device(drm_index *index, const float *d_x, int64_t n, int32_t k, 
 int drm_search_device_ex(drm_index *index, const float *d_x, int64_t n, int32_t k, int32_t ef, float *d_D,
                          int64_t *d_I, int32_t *d_ndis, int32_t *d_nhops, int32_t *d_nhops_upper, void *stream);
 /* Tuning (no reference counterpart): resident search waves per CU of this index's persistent search grid
- * (0 = the default, 20: every CU's LDS holds 20 PQ lookup tables of 8 KB). Fewer leave room on every CU
- * for a rerank kernel running beside the search on another stream (drm_refs_set_sw_waves). Results do
- * not depend on it. */
+ * (0 = the default, 20: every CU's LDS holds 20 PQ lookup tables of 8 KB). Used by the occupancy scans of
+ * DESIGN.md sec. 4.1. Results do not depend on it. */
 int drm_index_set_search_waves(drm_index *index, int32_t waves_per_cu);
 /* Statistics (no reference counterpart): on (1), ndis counts faiss's HNSWStats.ndis exactly -- the links each
  * hop finds not yet visited -- with a per-slot visited bitmap kept beside the search (the lean kernel needs none
  * for its results). Off (0, the default; DRM_SEARCH_EXACT_STATS=1 at load sets it) the lean
  * kernel reports the distances it computed. Results (D, I, nhops) do not depend on it. */
 int drm_index_set_exact_stats(drm_index *index, int32_t on);
-/* Diagnostic (no reference counterpart): how many queries of the last search on this index met an
- * exact distance tie and were re-run by the exact (faiss heap-layout) kernel. Synchronizes the device. */
-int drm_search_fallbacks(drm_index *index, int64_t *count);
+/* Safety (no reference counterpart): every search kernel bounds its loops -- a query past ntotal level-0 hops, or
+ * a persistent wave past n work items, means broken search state, and ends with nhops = ndis = -1 for the query
+ * and an error count instead of a hang. drm_search returns DRM_ERR_INTERNAL when the count
+ * is non-zero; callers of the device entry points (drm_search_device[_ex]) read it here. Synchronizes the
+ * device and resets the count. */
+int drm_index_search_errors(drm_index *index, int64_t *count);
 
 /* ---------------------------------------------------------------- fp32-L2 index (hnswlib)
  * The reference's hnswlib backend (BASELINE configs[1] "HIP L2 HNSW
@@ -156,9 +173,8 @@ int drm_flat_search_device(drm_flat_index *index, const float *d_x, int64_t n, i
 /* Diagnostic: queries of the last search whose candidate_set outgrew the GPU heap (their outputs
  * are invalid; drm_flat_search reports it as an error). Synchronizes the device. */
 int drm_flat_search_overflows(drm_flat_index *index, int64_t *count);
-/* Diagnostic: queries of the last search that the tie-free sorted-array pass handed to the exact
- * heap-replay pass (a distance tie among top_candidates). Synchronizes the device. */
-int drm_flat_search_fallbacks(drm_flat_index *index, int64_t *count);
+/* As drm_index_search_errors for the fp32 index (drm_flat_search returns DRM_ERR_INTERNAL on a non-zero count). */
+int drm_flat_search_errors(drm_flat_index *index, int64_t *count);
 
 /* ---------------------------------------------------------------- Smith-Waterman rerank */
 /* Batched calc_sw_score(seq1, seq2) (includes/utils/metrics.hpp:22, src/utils/metrics.cpp:10-45):
@@ -182,10 +198,6 @@ int drm_refs_is_genome(const drm_refs *refs, int *is_genome);
  * and only A/C/G/T/N kept (from every later line, headers included -- the reference's behaviour).
  * Two calls: *len receives the length (out may be NULL), then out[0 .. *len) the sequence. */
 int drm_extract_fasta_sequence(const char *path, uint8_t *out, int64_t *len);
-/* Tuning (no reference counterpart): cap the SW score kernel's grid at waves_per_cu resident waves per CU
- * (0 = uncapped: one wave per query up to 65536). Used to run the rerank of one batch beside the search of
- * the next on the same CUs (drm_index_set_search_waves). Results do not depend on it. */
-int drm_refs_set_sw_waves(drm_refs *refs, int32_t waves_per_cu);
 /* Shape and device of a window table (any out-pointer may be NULL). */
 int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device);
 
@@ -281,22 +293,20 @@ int drm_search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t 
                       drm_search_stats *stats);
 
 /* The same search -> SW rerank on DEVICE-resident buffers (shapes as drm_search_rerank; d_ndis, d_nhops,
- * d_nhops_upper may be NULL), enqueued behind the caller's work on `stream` and joined back into it. The n
- * queries run as DRM_CO_BATCHES batches (default 1) on two internal streams, search(b) beside rerank(b-1) on the
- * same CUs with capped grids (DRM_CO_SEARCH_WAVES = 8 search and DRM_CO_SW_WAVES = 4 rerank waves per CU), so the
- * rerank's VALU work can fill issue slots the memory-bound search leaves idle (measured: no faster at C5 on
- * MI355X, DESIGN.md sec. 5 -- hence one batch by default: the search, then the rerank, each with the whole chip).
- * The outputs equal those of drm_search_device + drm_post_process_sw_static_device (or _dynamic_device for a
- * genome handle) over the whole batch. d_status must be checked by the caller. stats (may be NULL) makes the call
- * synchronous and returns the device span and the summed search / rerank launch spans. */
+ * d_nhops_upper may be NULL), enqueued on `stream`: the search, then the rerank, each with the whole chip
+ * (co-scheduling them on shared CUs measured slower at C5 and was removed in round 5). The
+ * outputs equal those of drm_search_device + drm_post_process_sw_static_device (or _dynamic_device for a genome
+ * handle). d_status must be checked by the caller, and search errors read with drm_index_search_errors. stats
+ * (may be NULL) makes the call synchronous and returns the device span and the search / rerank spans
+ * (n_batches = 1; first_search_ms = search_ms, last_sw_ms = sw_ms). */
 typedef struct {
     int64_t nq;
     int32_t n_batches;
     double kernel_ms;       /* device span: first search start -> last rerank end */
-    double search_ms;       /* sum of the search launches' spans (overlapped ones included) */
-    double sw_ms;           /* sum of the rerank launches' spans */
-    double first_search_ms; /* the first search, alone on the device */
-    double last_sw_ms;      /* the last rerank, alone on the device */
+    double search_ms;       /* the search's span */
+    double sw_ms;           /* the rerank's span */
+    double first_search_ms; /* = search_ms (one batch) */
+    double last_sw_ms;      /* = sw_ms (one batch) */
 } drm_pipeline_stats;
 int drm_search_rerank_device(drm_index *index, drm_refs *refs, const float *d_x, int64_t n, int32_t k_clusters,
                              int32_t ef, const uint8_t *d_queries, const int32_t *d_q_len, int32_t q_stride,

@@ -77,7 +77,7 @@ def _verdict_worker(rank, world, port, mode, out_path):
     D = bench.Dist()
     good = {"backend": "RCCL", "ms": 1.0, "rows": 10}
     if rank == 0:
-        good["rank0_shard_matches"] = mode != "mismatch"
+        good["shards_match"] = [True, mode != "mismatch"]
     gather = {"error": "RuntimeError: forced"} if (mode == "error" and rank == 1) else (
         {"skipped": "2 ranks share 1 device(s)"} if mode == "skipped" else good)
     v = bench.gather_verdict(D, gather)
@@ -88,7 +88,7 @@ def _verdict_worker(rank, world, port, mode, out_path):
 
 @pytest.mark.parametrize("mode,expect", [("ok", True), ("error", False), ("mismatch", False), ("skipped", None)])
 def test_bench_gather_verdict_two_ranks(tmp_path, mode, expect):
-    """bench.py at N > 1: a gather error on any rank (here rank 1 only) or a rank-0 shard mismatch fails the job on
+    """bench.py at N > 1: a gather error on any rank (here rank 1 only) or a shard mismatch fails the job on
     every rank (gather_ok false, non-zero exit); a gather skipped because ranks share a device is not checked."""
     import json
     import torch.multiprocessing as mp
@@ -96,3 +96,72 @@ def test_bench_gather_verdict_two_ranks(tmp_path, mode, expect):
     mp.spawn(_verdict_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
     for r in range(2):
         assert json.load(open(f"{out}.{r}")) == expect
+
+
+def _checksum_worker(rank, world, port, shift, out_path):
+    """One rank of a gloo job: its result rows (seeded, distinct per rank) are 'gathered' to rank 0 with rank 1's
+    rows placed `shift` rows off their range, then verified as bench.py does (bench.shard_checksums on every rank's
+    own checksum against rank 0's checksum of that rank's range of the gathered rows, then bench.gather_verdict)."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    from deepreadmapper_amd.device import host_checksum
+    from deepreadmapper_amd.shard import shard_range
+    D = bench.Dist()
+    n_total = 1001
+    lo, hi = shard_range(n_total, rank, world)
+    rows = {"sw_ids": np.random.default_rng(rank).integers(0, 1 << 40, (hi - lo, 16)).astype(np.uint64),
+            "sw_scores": np.random.default_rng(10 + rank).integers(0, 150, (hi - lo, 16)).astype(np.int32)}
+    parts = [None] * world
+    D.dist.all_gather_object(parts, rows)  # stands in for the RCCL gather: rank 0 assembles the rows
+    full = None
+    if rank == 0:
+        full = {k: np.zeros((n_total, 16), v.dtype) for k, v in rows.items()}
+        for r in range(world):
+            rl, rh = shard_range(n_total, r, world)
+            d0 = rl + (shift if r == 1 else 0)  # where rank r's rows land
+            j0, j1 = max(d0, 0), min(d0 + rh - rl, n_total)
+            for k in full:
+                full[k][j0:j1] = parts[r][k][j0 - d0:j1 - d0]
+    local = {k: host_checksum(v) for k, v in rows.items()}
+    match = bench.shard_checksums(D, n_total, local, lambda a, b: {k: host_checksum(v[a:b]) for k, v in full.items()})
+    gather = {"backend": "gloo stand-in", "rows": n_total}
+    if rank == 0:
+        gather["shards_match"] = match
+    v = bench.gather_verdict(D, gather)
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump({"ok": v, "match": match}, f)
+    D.close()
+
+
+@pytest.mark.parametrize("shift,expect", [(0, True), (1, False), (-1, False)])
+def test_bench_gather_checksums_every_rank(tmp_path, shift, expect):
+    """bench.py's gather check covers every rank's rows: rank 1's rows one row off their range (a wrong offset in
+    the gather) make gather_ok false on every rank, with rank 0's match list naming rank 1."""
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "c")
+    mp.spawn(_checksum_worker, args=(2, _free_port(), shift, out), nprocs=2, join=True)
+    for r in range(2):
+        got = json.load(open(f"{out}.{r}"))
+        assert got["ok"] == expect
+    assert json.load(open(f"{out}.0"))["match"][1] == expect  # (shift -1 also overwrites rank 0's last row)
+
+
+def test_host_checksum_properties():
+    """drm_device_checksum's host form: position-dependent (swapped words, a shifted row, a changed byte in the
+    zero-padded tail all change it), and the empty buffer sums to 0."""
+    from deepreadmapper_amd.device import host_checksum
+    a = np.random.default_rng(3).integers(0, 1 << 62, 1000).astype(np.int64)
+    b = a.copy()
+    b[[10, 11]] = b[[11, 10]]
+    assert host_checksum(a) != host_checksum(b)
+    assert host_checksum(a[1:]) != host_checksum(a[:-1])
+    t = np.arange(13, dtype=np.uint8)
+    t2 = t.copy()
+    t2[12] ^= 1
+    assert host_checksum(t) != host_checksum(t2)
+    assert host_checksum(np.zeros(0, np.uint8)) == 0

@@ -1,8 +1,7 @@
 """GPU parity of the fp32-L2 hnswlib kernel (hnsw_flat_search.hip) against the oracle restatement
 (oracle/hnswlib_oracle.cpp, libstdc++'s own priority_queue): labels, fp32 distances (0 ulp, same op
-order) and ndis/nhops bit-exact, including an index full of exact distance ties. The default launch
-is the exact heap replay; with DRM_SEARCH_SORTED=1 a tie-free sorted-array pass runs first and hands
-tied queries to the replay -- both configurations are checked."""
+order) and ndis/nhops bit-exact, including an index full of exact distance ties (the launch is the exact heap
+replay; the opt-in tie-free sorted-array pass was removed in round 5)."""
 import numpy as np
 import pytest
 
@@ -20,9 +19,9 @@ def _both(index_path, fx, q, k, ef):
     assert np.array_equal(L.astype(np.int64)[~pad], Io[~pad]) and (L[pad] == np.uint64(2 ** 64 - 1)).all()
     assert np.array_equal(D.view(np.uint32), Do.view(np.uint32))  # 0 ulp
     assert st.ndis == int(nd.sum()) and st.nhops == int(nh.sum())
-    fb = ix.fallbacks()
+    assert ix.search_errors() == 0
     ix.free()
-    return D, L, fb
+    return D, L
 
 
 @pytest.mark.parametrize("k,ef", [(128, 128), (10, 64), (1, 1), (200, 100), (32, 400)])
@@ -31,22 +30,7 @@ def test_flat_c1_bitexact(c1_flat, k, ef):
 
 
 def test_flat_syn20k_bitexact(syn_flat):
-    _, _, fb = _both(syn_flat["index"], syn_flat["fx"], syn_flat["q"], 128, 128)
-    assert fb == 0  # default: exact replay only
-
-
-def test_flat_sorted_pass(syn_flat, c1_flat, rep_flat, monkeypatch):
-    """tie-free sorted-array pass + hand-over of tied queries (DRM_SEARCH_SORTED=1)"""
-    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
-    rng = np.random.default_rng(9)
-    q = rng.standard_normal((300, 128)).astype(np.float32)
-    _, _, fb = _both(syn_flat["index"], syn_flat["fx"], q, 128, 128)
-    assert fb < len(q)  # random queries meet few ties: most finish in the sorted pass
     _both(syn_flat["index"], syn_flat["fx"], syn_flat["q"], 128, 128)
-    for k, ef in [(10, 64), (1, 1), (200, 100), (64, 256)]:
-        _both(c1_flat["index"], c1_flat["fx"], c1_flat["q"], k, ef)
-    _, _, fb = _both(rep_flat["index"], rep_flat["fx"], rep_flat["q"], 64, 128)
-    assert fb > 0  # identical vectors: the exact pass took over
 
 
 def test_flat_ties_bitexact(rep_flat):

@@ -264,24 +264,12 @@ def test_search_committed_c1_fixture():
     assert np.array_equal(I, exp["I"]) and np.array_equal(D.view(np.uint32), exp["D"].view(np.uint32))
 
 
-def test_search_syn20k_sorted_pass(syn20k, monkeypatch):
-    """The opt-in sorted-array pass + exact fallback equals the oracle on the dense index."""
-    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
-    w = syn20k["w"]
-    _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
-
-
 @pytest.mark.parametrize("k,ef", [(128, 128), (16, 64), (100, 128)])
-def test_search_ties_fallback(repeats, k, ef, monkeypatch):
-    """Repeated genome segments give identical PQ codes: the sorted-array pass (DRM_SEARCH_SORTED=1)
-    must hand those queries to the exact kernel, and the merged output must still equal the oracle."""
-    from deepreadmapper_amd import read_index
-    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
+def test_search_ties_exact_kernel(repeats, k, ef, monkeypatch):
+    """Repeated genome segments give identical PQ codes: the general exact kernel (DRM_SEARCH_FAST=0) replays
+    faiss's heap layout through the ties and equals the oracle."""
+    monkeypatch.setenv("DRM_SEARCH_FAST", "0")
     _search_both(repeats["index"], repeats["fx"], repeats["q"], k, ef)
-    ix = read_index(repeats["index"])
-    ix.search(repeats["q"], k, ef)
-    nfb = ix.fallbacks()
-    assert 0 < nfb <= len(repeats["q"])
 
 
 @pytest.mark.parametrize("fast", ["1", "0"])
@@ -309,12 +297,35 @@ def test_search_syn20k_exact_kernel(syn20k, monkeypatch):
     _search_both(syn20k["index"], syn20k["fx"], w.q_emb, 128, 128)
 
 
-def test_search_exact_kernel_forced(syn20k, monkeypatch):
-    """DRM_SEARCH_SORTED=1 with DRM_SEARCH_EXACT=1 (read at index load): exact kernel only."""
-    monkeypatch.setenv("DRM_SEARCH_SORTED", "1")
-    monkeypatch.setenv("DRM_SEARCH_EXACT", "1")
-    w = syn20k["w"]
-    _search_both(syn20k["index"], syn20k["fx"], w.q_emb[:700], 128, 128)
+@pytest.mark.parametrize("kernel", ["lean", "exact", "lds", "flat"])
+def test_search_bounds_fail_loudly(syn20k, c1_flat, kernel, monkeypatch):
+    """Every search kernel family bounds its loops: lowered through the load-time knobs, a
+    query past the level-0 hop bound (DRM_SEARCH_HOP_BOUND) and a persistent wave past its work-item bound
+    (DRM_WAVE_ITEM_BOUND) end with DRM_ERR_INTERNAL from the search instead of looping; the default bounds (ntotal
+    hops, n items) never trigger."""
+    from deepreadmapper_amd import HnswFlatIndex, read_index
+    from deepreadmapper_amd._native import DrmError
+    monkeypatch.setenv("DRM_SEARCH_FAST", "0" if kernel == "exact" else "1")
+    monkeypatch.setenv("DRM_SEARCH_LDS_KERNEL", "1" if kernel == "lds" else "0")
+    if kernel == "flat":
+        path, q = c1_flat["index"], c1_flat["q"]
+        load = lambda: HnswFlatIndex(path)  # noqa: E731
+    else:
+        path, q = syn20k["index"], syn20k["w"].q_emb
+        load = lambda: read_index(path)  # noqa: E731
+    q = np.ascontiguousarray(np.resize(q, (12_000, q.shape[1])))  # more queries than resident waves
+    ix = load()
+    ix.search(q, 32, 64)  # the natural bounds: no error
+    ix.free()
+    for knob, val in (("DRM_SEARCH_HOP_BOUND", "2"), ("DRM_WAVE_ITEM_BOUND", "1")):
+        monkeypatch.setenv(knob, val)
+        ix = load()
+        with pytest.raises(DrmError) as e:
+            ix.search(q, 32, 64)
+        assert e.value.code == -8, str(e.value)  # DRM_ERR_INTERNAL
+        assert ix.search_errors() == 0  # reported once, then reset
+        ix.free()
+        monkeypatch.delenv(knob)
 
 
 def test_search_device_stats(syn20k):

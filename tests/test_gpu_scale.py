@@ -169,17 +169,13 @@ def test_c4_sparse_rerank(c4):
         _check_rerank(refs, I, w.queries[:20_000], 4, k, kc)
 
 
-@pytest.mark.parametrize("batches,sw_waves", [(4, 4), (3, 2), (1, 4)])
-def test_c3_coscheduled_device_pipeline(c3, monkeypatch, batches, sw_waves):
-    """drm_search_rerank_device (the search of batch b beside the SW rerank of batch b-1, capped grids sharing
-    the CUs) gives byte-identical outputs to drm_search_device + drm_post_process_sw_static_device over the
-    whole C3 batch (100k reads), for several batch counts and grid caps."""
+def test_c3_device_pipeline(c3):
+    """drm_search_rerank_device (the search, then the SW rerank, on device buffers) gives byte-identical outputs to
+    drm_search_device + drm_post_process_sw_static_device over the whole C3 batch (100k reads)."""
     from deepreadmapper_amd import read_index, WindowTable
     from deepreadmapper_amd.device import DeviceBuffer, synchronize
     from deepreadmapper_amd.executor import search_rerank_device
     from deepreadmapper_amd._native import check, lib
-    monkeypatch.setenv("DRM_CO_BATCHES", str(batches))
-    monkeypatch.setenv("DRM_CO_SW_WAVES", str(sw_waves))
     w = c3["w"]
     K = 128
     Q = len(w.q_emb)
@@ -197,7 +193,7 @@ def test_c3_coscheduled_device_pipeline(c3, monkeypatch, batches, sw_waves):
             st = search_rerank_device(ix, table, d_x, Q, d_q, d_ql, q.shape[1], b["D"], b["I"], b["sc"], b["id"],
                                       b["st"], k=K, ef=128, d_ndis=b["nd"], d_nhops=b["nh"], d_nhops_upper=b["nu"],
                                       stats=True)
-            assert st.n_batches == batches and st.kernel_ms > 0 and st.search_ms > 0 and st.sw_ms > 0
+            assert st.n_batches == 1 and st.kernel_ms > 0 and st.search_ms > 0 and st.sw_ms > 0
         else:
             ix.search_device(d_x, Q, K, 128, b["D"], b["I"], b["nd"], b["nh"], d_nhops_upper=b["nu"])
             check(lib().drm_post_process_sw_static_device(table.handle, b["I"].ptr, Q, K, d_q.ptr, d_ql.ptr, q.shape[1],

@@ -77,7 +77,7 @@ int main(int argc, char **argv)
                     hp.pop(kc); hp.push(kc, pack(key, id), id); root = hp.R[63]; rootI = hp.IR[63];
                 }
             } else if (n == 128) {
-                ++kc; root = hp.push_fill(kc, pack(key, id), id, pc, root, rootI);
+                ++kc; hp.push_fill(kc, pack(key, id), id, pc); root = hp.R[63]; rootI = hp.IR[63];
             } else {
                 ++kc; hp.push(kc, pack(key, id), id); root = hp.R[63]; rootI = hp.IR[63];
             }

@@ -80,11 +80,14 @@ extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t
                 const u32 key = dall[l]; const int32_t idl = v1[l];
                 if (hp.holds(idl)) continue;
                 ++kc;
-                root = hp.push_fill(kc, pack(key, idl), idl, pc, root, rootI);
+                hp.push_fill(kc, pack(key, idl), idl, pc);
                 ++nvalid;
                 pushed.push_back(idl);
             }
-            if (kc == ef) rem &= below_root();
+            if (kc == ef) { // the root is read once the heap is full (push_fill does not track it)
+                root = hp.R[63]; rootI = hp.IR[63];
+                rem &= below_root();
+            }
         } else {
             rem &= below_root();
         }
@@ -101,7 +104,7 @@ extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t
             if (evk == hi32(root)) lg.push_back(pack(evk, evi));
             pushed.push_back(idl);
         }
-        if (hp.R[63] != root || hp.IR[63] != rootI) { std::printf("root not current at hop %d\n", nstep); return -4; }
+        if (kc == ef && (hp.R[63] != root || hp.IR[63] != rootI)) { std::printf("root not current at hop %d\n", nstep); return -4; }
         maxlog = std::max<int>(maxlog, (int)lg.size());
         nstep++;
     }

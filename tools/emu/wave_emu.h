@@ -22,21 +22,34 @@ static u32 lo32(u64 v) { return (u32)v; }
 static bool sgt64(u64 a, u64 b) { return a > b; }
 
 struct PathConst {
-    u32 Alo[W], Auplo[W], Lreqlo[W], addrL[W], addrR[W], addrHalf[W], c2[W], bl[W], addrF[W];
+    // lane p holds the children of node p: slot 2p+1 (L, 1-based position 2p+2) and slot 2p+2 (R, 2p+3); lane 63's R
+    // is the root (1-based position 1). xL / xR / blL / blR: those positions and their bit lengths; addrF: the lane
+    // holding this lane's father slot p (its L half when p is odd, its R half when p is even; lane 63's R for p = 0)
+    u32 Alo[W], Ahi[W], Auplo[W], Lreqlo[W], addrL[W], addrR[W], addrHalf[W], xL[W], xR[W], blL[W], blR[W], addrF[W];
+    // replace128: the chain index of each half on slot 127's ancestor chain (127 = 0, 63 = 1, ..., 1 = 6, the root 7;
+    // 15 = not on it)
+    u32 cidxL[W], cidxR[W];
     PathConst() {
         for (int lane = 0; lane < W; ++lane) {
             addrL[lane] = (u32)((2 * lane + 1) & 63); addrR[lane] = (u32)((2 * lane + 2) & 63);
-            addrHalf[lane] = (u32)(lane >> 1); c2[lane] = 2u * lane + 2u; bl[lane] = bitlen(2u * lane + 2u);
-            addrF[lane] = lane > 0 ? (u32)((lane - 1) >> 1) : 0u;
+            addrHalf[lane] = (u32)(lane >> 1);
+            xL[lane] = 2u * lane + 2u; blL[lane] = bitlen(2u * lane + 2u);
+            xR[lane] = lane == 63 ? 1u : 2u * lane + 3u; blR[lane] = lane == 63 ? 1u : blL[lane];
+            addrF[lane] = lane > 0 ? (u32)((lane - 1) >> 1) : 63u;
+            cidxL[lane] = ((lane + 1) & lane) == 0 ? 6u - (u32)(31 - __builtin_clz((u32)lane + 1u)) : 15u;
+            cidxR[lane] = lane == 63 ? 7u : 15u;
             u64 A = 1ull << lane, Aup = 0, Lreq = 0;
             for (int c = lane; c > 0;) { int a = (c - 1) >> 1; A |= 1ull << a; Aup |= 1ull << a; if (c & 1) Lreq |= 1ull << a; c = a; }
-            Alo[lane] = (u32)A; Auplo[lane] = (u32)Aup; Lreqlo[lane] = (u32)Lreq;
+            Alo[lane] = (u32)A; Ahi[lane] = (u32)(A >> 32); Auplo[lane] = (u32)Aup; Lreqlo[lane] = (u32)Lreq;
         }
     }
+    // the lanes on the sift-down path: p and all its ancestors have mv set, and every ancestor chose the child toward
+    // p (lm: the nodes that take their L child) -- one per-lane test, one ballot
     u64 path(u64 mv, u64 lm) const {
-        bool p1[W], p2[W];
-        for (int l = 0; l < W; ++l) { p1[l] = ((u32)mv & Alo[l]) == Alo[l]; p2[l] = ((u32)lm & Auplo[l]) == Lreqlo[l]; }
-        return ballot(p1) & (mv | 0xFFFFFFFFull) & ballot(p2);
+        bool p[W];
+        for (int l = 0; l < W; ++l)
+            p[l] = ((~(u32)mv & Alo[l]) | (((u32)lm ^ Lreqlo[l]) & Auplo[l]) | (~(u32)(mv >> 32) & Ahi[l])) == 0u;
+        return ballot(p);
     }
 };
 
@@ -44,9 +57,8 @@ struct Heap {
     u64 L[W], R[W];
     int32_t IL[W], IR[W];
     bool holds(int32_t v) const { for (int l = 0; l < W; ++l) if (IL[l] == v || IR[l] == v) return true; return false; }
-    // Heap::replace128, straight-line (every case a lane mask; lane 63's R / IR hold the root on return)
+    // Heap::replace128 (lane-mask form, the root's bookkeeping in lane 63's R): returns the new root's key
     u64 replace128(u64 vnew, int32_t vnewI, const PathConst &pc, int32_t &rootI) {
-        constexpr u64 kHold = (1ull << 63) | (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const u64 val = L[63]; const int32_t valI = IL[63];
         bool t[W];
         for (int l = 0; l < W; ++l) t[l] = L[l] > R[l];
@@ -58,62 +70,55 @@ struct Heap {
         for (int l = 0; l < W; ++l) t[l] = !(val > chv[l]);
         const u64 mv = ballot(t);
         const u64 Wm = pc.path(mv, lm);
-        const int last = 63 - __builtin_clzll(Wm | 1ull);
-        const bool r0 = (Wm & 1ull) != 0ull;
-        const u64 rootv = r0 ? chv[0] : val; const int32_t rI = r0 ? chI[0] : valI;
-        const u64 wlm = Wm & lm, wrm = Wm & ~lm;
+        const u64 wlm = Wm & lm;
         u64 fl[W]; int32_t flI[W];
+        // lane 0: the root after the pop (node 0's chosen child if node 0 is on the path); lane 63 takes it (DPP rotate)
+        const bool on0 = (Wm & 1ull) != 0ull;
+        const u64 rootpp = on0 ? chv[0] : val; const int32_t rootppI = on0 ? chI[0] : valI;
         for (int l = 0; l < W; ++l) {
             const u32 half = (u32)l >> 1;
-            const bool moved = (((u32)wlm >> half) & 1u) != 0u, klast = half == (u32)last;
+            const bool atlast = (Wm >> l) == 1ull, klast = (Wm >> half) == 1ull, moved = ((wlm >> half) & 1ull) != 0ull;
             fl[l] = moved ? (klast ? val : chv[l]) : fpre[l]; flI[l] = moved ? (klast ? valI : chI[l]) : fpreI[l];
-            const bool atlast = l == last;
+            if (l == 0) { fl[l] = rootpp; flI[l] = rootppI; } // the chain's top father: the root
             const u64 up = atlast ? val : up0[l]; const int32_t upI = atlast ? valI : up0I[l];
             if ((wlm >> l) & 1) { L[l] = up; IL[l] = upI; }
-            if ((wrm >> l) & 1) { R[l] = up; IR[l] = upI; }
+            if (((Wm & ~lm) >> l) & 1) { R[l] = up; IR[l] = upI; }
         }
-        for (int l = 0; l < W; ++l) t[l] = vnew > (l == 63 ? rootv : L[l]);
-        const int h = __builtin_popcountll(ballot(t) & kHold);
-        fl[0] = rootv; flI[0] = rI;
-        const u64 shm = h ? kHold & (~0ull << ((1u << (7 - h)) - 1u)) : 0ull;
-        const u64 xm = h < 7 ? 1ull << ((1u << (6 - h)) - 1u) : 0ull;
+        R[63] = rootpp; IR[63] = rootppI;
+        for (int l = 0; l < W; ++l) t[l] = vnew > (pc.cidxR[l] == 7u ? R[l] : (pc.cidxL[l] != 15u ? L[l] : ~0ull));
+        const u32 h = (u32)__builtin_popcountll(ballot(t));
         for (int l = 0; l < W; ++l) {
-            if ((shm >> l) & 1) { L[l] = fl[l]; IL[l] = flI[l]; }
-            if ((xm >> l) & 1) { L[l] = vnew; IL[l] = vnewI; }
+            if (pc.cidxL[l] < h) { L[l] = fl[l]; IL[l] = flI[l]; }
+            if (pc.cidxL[l] == h) { L[l] = vnew; IL[l] = vnewI; }
+            if (pc.cidxR[l] == h) { R[l] = vnew; IR[l] = vnewI; }
         }
-        const u64 nroot = h == 7 ? vnew : rootv;
-        rootI = h == 7 ? vnewI : rI;
-        R[63] = nroot; IR[63] = rootI;
-        return nroot;
+        rootI = IR[63];
+        return R[63];
     }
-    u64 push_fill(int k, u64 val, int32_t valI, const PathConst &pc, u64 rootv, int32_t &rootI) {
-        const u32 s1 = (u32)k; const int B = bitlen(s1);
+    // heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128), lane-mask form: each half finds its chain
+    // index (1-based position x is on the chain of k at index m iff k >> m == x, m = bitlen(k) - bitlen(x)), the
+    // ancestors below val are a bottom prefix of length h, the halves of index < h take their father's value and the
+    // half of index h takes val. The root (lane 63's R) is the chain's last index. The root is not tracked here.
+    void push_fill(int k, u64 val, int32_t valI, const PathConst &pc) {
+        const u32 B = (u32)bitlen((u32)k);
+        u64 f[W]; int32_t fI[W]; u32 ciL[W], ciR[W];
         bool a1[W], a2[W];
-        for (int l = 0; l < W; ++l) { int m = B - (int)pc.bl[l]; u32 t = m >= 0 ? (s1 >> m) : 0u; a1[l] = t == pc.c2[l]; a2[l] = t == pc.c2[l] + 1u; }
-        const u64 OL = ballot(a1), OR = ballot(a2);
-        const u32 sl = (s1 - 2u) >> 1;
-        const u64 selfL = (s1 & 1u) ? 0ull : (1ull << sl), selfR = (s1 & 1u) ? (1ull << sl) : 0ull;
-        for (int l = 0; l < W; ++l) { a1[l] = val > L[l]; a2[l] = val > R[l]; }
-        const int h = __builtin_popcountll(ballot(a1) & OL & ~selfL) + __builtin_popcountll(ballot(a2) & OR & ~selfR) + (sgt64(val, rootv) ? 1 : 0);
-        if (h > 0) {
-            u64 f[W]; int32_t fI[W];
-            for (int l = 0; l < W; ++l) { bool odd = l & 1; f[l] = odd ? L[pc.addrF[l]] : R[pc.addrF[l]]; fI[l] = odd ? IL[pc.addrF[l]] : IR[pc.addrF[l]]; }
-            const u64 mlt = ~0ull << ((1u << (B - h - 1)) - 1u);
-            for (int l = 0; l < W; ++l) {
-                if (((OL & mlt) >> l) & 1) { L[l] = f[l]; IL[l] = fI[l]; }
-                if (((OR & mlt) >> l) & 1) { R[l] = f[l]; IR[l] = fI[l]; }
-            }
-            if (h == B - 1) {
-                if (OL & 1ull) { L[0] = rootv; IL[0] = rootI; }
-                if (OR & 1ull) { R[0] = rootv; IR[0] = rootI; }
-                rootI = valI;
-                R[63] = val; IR[63] = valI;
-                return val;
-            }
+        for (int l = 0; l < W; ++l) {
+            const u32 s = pc.addrF[l]; const bool odd = l & 1;
+            f[l] = odd ? L[s] : R[s]; fI[l] = odd ? IL[s] : IR[s];
+            const u32 mL = B - pc.blL[l], mR = B - pc.blR[l]; // wraps when negative: the 64-bit shift then gives 0
+            const u64 tL = (u64)(u32)k >> (mL & 63u), tR = (u64)(u32)k >> (mR & 63u);
+            ciL[l] = tL == pc.xL[l] ? mL : 99u; ciR[l] = tR == pc.xR[l] ? mR : 99u;
+            a1[l] = val > ((ciL[l] - 1u) < 7u ? L[l] : ~0ull);
+            a2[l] = val > ((ciR[l] - 1u) < 7u ? R[l] : ~0ull);
         }
-        const u32 x = (s1 >> h) - 1u; const int xl = (int)((x - 1u) >> 1);
-        if (x & 1u) { L[xl] = val; IL[xl] = valI; } else { R[xl] = val; IR[xl] = valI; }
-        return rootv;
+        const u32 h = (u32)(__builtin_popcountll(ballot(a1)) + __builtin_popcountll(ballot(a2)));
+        for (int l = 0; l < W; ++l) {
+            if (ciL[l] < h) { L[l] = f[l]; IL[l] = fI[l]; }
+            if (ciL[l] == h) { L[l] = val; IL[l] = valI; }
+            if (ciR[l] < h) { R[l] = f[l]; IR[l] = fI[l]; }
+            if (ciR[l] == h) { R[l] = val; IR[l] = valI; }
+        }
     }
     // general heap_pop(k) / heap_push(k, val) (ef < 128): Heap::pop / Heap::push of the kernel, lane by lane
     u64 get(int s) const { if (s == 0) return R[63]; int o = (s - 1) >> 1; return (s & 1) ? L[o] : R[o]; }

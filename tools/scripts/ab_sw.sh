@@ -3,6 +3,6 @@
 set -o pipefail
 for i in 1 2; do
   for lib in "$@"; do
-    echo "== $lib"; DRM_LIB=$PWD/$lib timeout -k 10 200 python -u tools/scripts/sw_waves_probe.py --waves 0 --windows 2000000 || exit 1
+    echo "== $lib"; DRM_LIB=$PWD/$lib timeout -k 10 200 python -u tools/scripts/sw_probe.py --windows 2000000 || exit 1
   done
 done
