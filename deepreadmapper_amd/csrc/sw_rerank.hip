@@ -469,23 +469,26 @@ __device__ __forceinline__ int acgt_code(int c) // A,C,G,T -> 0..3, anything els
     return (((0x47544341u >> (8 * k)) & 0xFFu) == (uint32_t)c) ? k : -1;
 }
 __device__ __forceinline__ int acgt_byte(int k) { return k < 4 ? (int)((0x47544341u >> (8 * k)) & 0xFFu) : -1; }
+// pair-profile row of candidate codes (ka, kb) (sw_score_f16_kernel): the A/C/G/T pairs first, 4 ka + kb
+__device__ __forceinline__ int pair_row(int ka, int kb)
+{
+    return ka < 4 ? (kb < 4 ? 4 * ka + kb : 16 + ka) : (kb < 4 ? 20 + kb : 24);
+}
 
 // Kernel 1 (fast path) of the rerank: candidate lists (find_sequences static) + one SW score per
 // candidate; same contract as sw_score_kernel. One 64-lane workgroup per query (grid-stride).
 template <int LQ>
 __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
 {
-    // Pair-profile layout: row (ka, kb) at ka * GST + kb * PST words. A ds_read_b128 lane group (16
-    // lanes) is conflict-free when the 16-byte chunk index (address / 16) mod 16 differs between
-    // distinct rows; with PST / 4 = 7 or 1 (mod 16) and GST / 4 = 4 (mod 16) the 16 A/C/G/T pairs
-    // (ka, kb < 4) land on 16 distinct chunk indices (MI355X_MICROARCH.md, LDS banking).
+    // Pair-profile layout: the row of candidate codes (ka, kb) (0..3 = A, C, T, G; 4 = none) is row
+    // p = pair_row(ka, kb) at p * PST words: the 16 A/C/G/T pairs are p = 4 ka + kb = 0..15, the pairs with a
+    // 'none' code follow (16 + ka, 20 + kb, 24). A ds_read_b128 lane group (16 lanes) is conflict-free when the
+    // 16-byte chunk index (address / 16) mod 16 differs between distinct rows: with PST / 4 odd, p * PST / 4 mod 16
+    // is distinct for p = 0..15 (MI355X_MICROARCH.md, LDS banking). And p = 4 ka + kb of four rows at once is two
+    // byte-wise (SWAR) operations on the candidates' code words (the fast path below).
     constexpr int PST = ((LQ + 3) & ~3) + 4 + (((((LQ + 3) & ~3) + 4) / 4) % 2 == 0 ? 4 : 0);
-    constexpr int GST = 5 * PST + 4 * (((4 - 5 * (PST / 4)) % 16 + 16) % 16);
-    static_assert((PST / 4) % 2 == 1 && (GST / 4) % 16 == 4, "pair-profile bank spread");
-    // the last ka block needs only its 5 rows, not a full GST: with the candidate list sized to the call
-    // (dynamic LDS, a.cmax entries) a 152-byte query's workgroup fits 16 KB, so one SW wave per SIMD can sit
-    // beside three search waves (8 KB of LUT each) on a CU (co-resident search + rerank)
-    constexpr int PPROF = 4 * GST + 5 * PST;
+    static_assert((PST / 4) % 2 == 1, "pair-profile bank spread");
+    constexpr int PPROF = 25 * PST;
     __shared__ __align__(16) uint32_t pprof[PPROF];
     // the query as given (up to LQ + 2 bytes: the tags of a 150 bp read around LQ = 150 DP columns)
     constexpr int QB = (LQ + 2 + 15) & ~15;
@@ -545,8 +548,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
         }
         __syncthreads();
         const int lead = lead_s, qe = qe_s;
-        // one column per lane: its query byte is tested once against A, C, G, T and written to the 25 rows; the words
-        // between row blocks (GST - 5 * PST) are never read
+        // one column per lane: its query byte is tested once against A, C, G, T and written to the 25 rows
         for (int j = tid; j < PST; j += 64) {
             const int c = (j < qe && j < LQ) ? (int)qbuf[lead + j] : -1; // past the query: matches nothing
             // the diagonal term: +2 on a match (the -1 every cell takes makes it +1); code 4 matches nothing
@@ -559,7 +561,7 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
             for (int ka = 0; ka < 5; ++ka)
 #pragma unroll
                 for (int kb = 0; kb < 5; ++kb)
-                    pprof[ka * GST + kb * PST + j] = m[ka] | (m[kb] << 16);
+                    pprof[pair_row(ka, kb) * PST + j] = m[ka] | (m[kb] << 16);
         }
         __syncthreads();
         // longer than the buffer: unsupported here (-3); more than LQ columns left after the tags: the bit-profile
@@ -591,37 +593,12 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                 na4 = pa[0];
                 nb4 = pb[0];
             }
-            uint32_t wa4 = 0u, wb4 = 0u;
-            // profile row of DP row i (called for i = 0, 1, ... in order)
-            auto row = [&](int i) -> const uint32_t * {
-                int ca, cb;
-                if (a.genome) {
-                    ca = ra.at(i);
-                    cb = has_b ? rb.at(i) : -1;
-                } else {
-                    if ((i & 15) == 0) { // wave-uniform: next block becomes current, prefetch the one after
-                        ba = na4;
-                        bb = nb4;
-                        const int nx = (i >> 4) + 1;
-                        if (nx < nblk && 16 * nx < L) {
-                            na4 = pa[nx];
-                            nb4 = pb[nx];
-                        }
-                    }
-                    if ((i & 3) == 0) { // take the next word of the block (register moves, no indexing)
-                        wa4 = ba.x;
-                        wb4 = bb.x;
-                        ba = make_uint4(ba.y, ba.z, ba.w, 0u);
-                        bb = make_uint4(bb.y, bb.z, bb.w, 0u);
-                    } else {
-                        wa4 >>= 8;
-                        wb4 >>= 8;
-                    }
-                    ca = (int)(wa4 & 255u);
-                    cb = has_b ? (int)(wb4 & 255u) : -1;
-                }
+            // profile row of candidate bytes (ca, cb) (-1: past the window / no second candidate): a byte that is not
+            // A/C/G/T takes the 'none' code 4, unless the query holds it (e.g. N against N): the query is then flagged
+            // for the bit-profile kernel
+            auto prow = [&](int ca, int cb) -> const uint32_t * {
                 int ka = acgt_code(ca), kb = acgt_code(cb);
-                if (ka < 0) { // N (or the empty window, -1): "a byte the query lacks" unless it has it
+                if (ka < 0) {
                     flagged |= ca >= 0 && ((qmask[ca >> 5] >> (ca & 31)) & 1u) != 0u;
                     ka = 4;
                 }
@@ -629,19 +606,68 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
                     flagged |= cb >= 0 && ((qmask[cb >> 5] >> (cb & 31)) & 1u) != 0u;
                     kb = 4;
                 }
-                return pprof + ka * GST + kb * PST;
+                return pprof + pair_row(ka, kb) * PST;
             };
-            int i = 0;
-            for (; i + DRM_SW_ROWS <= L; i += DRM_SW_ROWS) {
-                const uint32_t *pr[DRM_SW_ROWS];
+            if (a.genome) {
+                // dynamic lookup: window bytes one at a time (reverse-complemented for odd ids)
+                int i = 0;
+                for (; i + DRM_SW_ROWS <= L; i += DRM_SW_ROWS) {
+                    const uint32_t *pr[DRM_SW_ROWS];
 #pragma unroll
-                for (int r = 0; r < DRM_SW_ROWS; ++r)
-                    pr[r] = row(i + r); // in row order: row() steps through the candidate bytes
-                sw_rows_i16<LQ, DRM_SW_ROWS, DRM_SW_PF>(H, pr, best);
-            }
-            for (; i < L; ++i) {
-                const uint32_t *pr[1] = {row(i)};
-                sw_rows_i16<LQ, 1, DRM_SW_PF>(H, pr, best);
+                    for (int r = 0; r < DRM_SW_ROWS; ++r)
+                        pr[r] = prow(ra.at(i + r), has_b ? rb.at(i + r) : -1);
+                    sw_rows_i16<LQ, DRM_SW_ROWS, DRM_SW_PF>(H, pr, best);
+                }
+                for (; i < L; ++i) {
+                    const uint32_t *pr[1] = {prow(ra.at(i), has_b ? rb.at(i) : -1)};
+                    sw_rows_i16<LQ, 1, DRM_SW_PF>(H, pr, best);
+                }
+            } else {
+                // static table: each 4-byte word of a candidate's 16-byte block holds 4 DP rows. Fast path: when every
+                // byte of the word is A/C/G/T in every lane, the codes of its 4 rows come from two byte-wise operations
+                // (k = (c >> 1) & 3, checked against the A/C/T/G table by one v_perm) and their profile rows are
+                // p = 4 ka + kb, one byte each of p4 -- a bit-field extract and a multiply-add per row instead of the
+                // per-row code tests
+                uint32_t wa4 = 0u, wb4 = 0u, p4 = 0u;
+                bool fast = false;
+                auto row = [&](int i) -> const uint32_t * {
+                    if ((i & 3) == 0) { // wave-uniform: the next word of each block (register moves, no indexing)
+                        if ((i & 15) == 0) { // the next block becomes current, prefetch the one after
+                            ba = na4;
+                            bb = nb4;
+                            const int nx = (i >> 4) + 1;
+                            if (nx < nblk && 16 * nx < L) {
+                                na4 = pa[nx];
+                                nb4 = pb[nx];
+                            }
+                        }
+                        wa4 = ba.x;
+                        wb4 = has_b ? bb.x : 0u;
+                        ba = make_uint4(ba.y, ba.z, ba.w, 0u);
+                        bb = make_uint4(bb.y, bb.z, bb.w, 0u);
+                        const uint32_t ka4 = (wa4 >> 1) & 0x03030303u, kb4 = (wb4 >> 1) & 0x03030303u;
+                        const uint32_t bad = (__builtin_amdgcn_perm(0u, 0x47544341u, ka4) ^ wa4) |
+                                             (has_b ? (__builtin_amdgcn_perm(0u, 0x47544341u, kb4) ^ wb4) : 0u);
+                        fast = i + 4 <= L && __ballot(bad != 0u) == 0ull;
+                        p4 = has_b ? (ka4 << 2) + kb4 : ka4 + 0x10101010u; // (ka, 'none'): 16 + ka
+                    }
+                    const uint32_t sh = 8u * (uint32_t)(i & 3);
+                    if (fast)
+                        return pprof + __builtin_amdgcn_ubfe(p4, sh, 8u) * PST;
+                    return prow((int)((wa4 >> sh) & 255u), has_b ? (int)((wb4 >> sh) & 255u) : -1);
+                };
+                int i = 0;
+                for (; i + DRM_SW_ROWS <= L; i += DRM_SW_ROWS) {
+                    const uint32_t *pr[DRM_SW_ROWS];
+#pragma unroll
+                    for (int r = 0; r < DRM_SW_ROWS; ++r)
+                        pr[r] = row(i + r); // in row order: row() steps through the candidate bytes
+                    sw_rows_i16<LQ, DRM_SW_ROWS, DRM_SW_PF>(H, pr, best);
+                }
+                for (; i < L; ++i) {
+                    const uint32_t *pr[1] = {row(i)};
+                    sw_rows_i16<LQ, 1, DRM_SW_PF>(H, pr, best);
+                }
             }
             const int score_a = (int)(best & 0xFFFFu), score_b = (int)(best >> 16);
             const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
