@@ -431,7 +431,25 @@ int drm_index_set_exact_stats(drm_index *index, int32_t on)
     return guarded([&] {
         if (!index)
             throw Error(DRM_ERR_ARG, "null index");
-        index->dev.exact_stats = on ? 1 : 0;
+        drm::DeviceIndex &d = index->dev;
+        d.exact_stats = on ? 1 : 0;
+        // switched off on an index whose searches take the lean kernel: the per-slot visited bitmap (32 GB at C5) was
+        // there for the count only -- release it (a search that needs it again, another kernel or exact statistics,
+        // allocates it anew)
+        if (!on && d.rows && d.visited) {
+            DRM_HIP_CHECK(hipSetDevice(d.device));
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            DRM_HIP_CHECK(hipFree(d.visited));
+            d.visited = nullptr;
+            d.device_bytes -= (int64_t)sizeof(uint32_t) * d.n_slots * d.vis_words;
+            if (d.clear_list) {
+                DRM_HIP_CHECK(hipFree(d.clear_list));
+                d.clear_list = nullptr;
+                d.device_bytes -= (int64_t)sizeof(int32_t) * d.n_slots * d.clear_cap;
+            }
+            d.n_slots = 0;
+            d.vis_words = 0;
+        }
     });
 }
 

@@ -139,7 +139,14 @@ struct ExecCache {
         // two non-blocking streams (no implicit synchronisation with the legacy null stream). HIP deals its
         // streams round-robin over GPU_MAX_HW_QUEUES hardware queues (4 on the box) and two streams on one queue
         // run in submission order (tools/microbench/concurrency.hip); the executor's own two streams are created
-        // together, so they land on different queues.
+        // together, so they land on different queues. Either may share its queue with a stream the process made
+        // earlier (the caller's, RCCL's, torch's). That is acceptable here: the executor orders itself behind the
+        // caller's stream anyway (an event at entry, the caller waits on ours at exit), RCCL and torch streams carry
+        // no work while a search runs in this library's callers (the bench's gather runs after its timed region),
+        // and a queue shared with an idle stream costs nothing. Round 3 gave each stream a queue of its own with a
+        // full CU mask (hipExtStreamCreateWithCUMask), but such streams synchronise with the null stream; round-3
+        // advice asked for non-blocking ones, and the measured overlap of search and rerank batches
+        // (profiles/r02/pipe_c3/timeline_2streams.txt) does not depend on it.
         for (hipStream_t *s : {&s_search, &s_sw})
             HC(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         HC(hipEventCreate(&e0));

@@ -194,12 +194,8 @@ struct Heap {
         const int o = (s - 1) >> 1;
         return (s & 1) ? readlane32(IL, o) : readlane32(IR, o);
     }
-    // node v is in the heap: one per-lane test (the smaller of the two id differences is 0) and one ballot
-    __device__ __forceinline__ bool holds(int32_t v) const
-    {
-        const uint32_t dl = (uint32_t)(IL ^ v), dr = (uint32_t)(IR ^ v);
-        return ballot((dl < dr ? dl : dr) == 0u) != 0ull;
-    }
+    // node v is in the heap (one compare per half, wave-uniform answer)
+    __device__ __forceinline__ bool holds(int32_t v) const { return (ballot(IL == v) | ballot(IR == v)) != 0ull; }
     // the root's key (high word) and node id
     __device__ __forceinline__ uint32_t root_hi() const { return (uint32_t)__builtin_amdgcn_readlane((int)hi32(R), 63); }
     __device__ __forceinline__ int32_t root_id() const { return readlane32(IR, 63); }
@@ -323,10 +319,12 @@ struct Heap {
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
-        // per-lane tests: the path is a chain of nodes, so its deepest node p is the one with W >> p == 1
-        const bool atlast = (W >> lane) == 1ull;
-        const bool klast = (W >> pc.half) == 1ull;
-        const bool moved = ((W & lm) >> pc.half) & 1ull; // lane (lane >> 1) is on the path and took its L child
+        // per-lane tests: the path is a chain of nodes, so its deepest node is W's highest bit (none: 64)
+        const uint32_t lastW = W ? 63u - (uint32_t)__builtin_clzll(W) : 64u;
+        const bool atlast = (uint32_t)lane == lastW;
+        const bool klast = pc.half == lastW;
+        // lane (lane >> 1) is on the path and took its L child (lane >> 1 < 32: the low word holds its bit)
+        const bool moved = ((uint32_t)(W & lm) >> pc.half) & 1u;
         // lane 0: the root after the pop -- node 0's chosen child if node 0 is on the path (lane 0's own bit of W),
         // else slot 127's value
         const bool onw = in_mask(W);
@@ -351,9 +349,10 @@ struct Heap {
         const int32_t nrootI = (int32_t)dpp_rol1_u32((uint32_t)rootppI);
         R = s63 ? nroot : R;
         IR = s63 ? nrootI : IR;
-        // push: h = the chain's ancestors below vnew after the pop (lane 63 stands for the root, index 7)
-        const uint64_t chain = s63 ? R : (pc.cidx < 15u ? L : ~0ull);
-        const uint32_t h = (uint32_t)__builtin_popcountll(ballot(vnew > chain));
+        // push: h = the chain's ancestors below vnew after the pop: the L halves of lanes 31, 15, 7, 3, 1, 0 (slots 63 ..
+        // 1) and lane 63's R (the root, index 7)
+        constexpr uint64_t kChainL = (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
+        const uint32_t h = (uint32_t)__builtin_popcountll((ballot(vnew > L) & kChainL) | (ballot(vnew > R) & (1ull << 63)));
         // the chain indices below h take their father's value, index h takes vnew (h = 7: the root)
         const bool sh = pc.cidx < h;
         L = sh ? fl : L;
@@ -383,9 +382,9 @@ struct Heap {
         const uint32_t t = (uint32_t)((uint64_t)k >> (m & 63u));
         const uint32_t ciL = t == pc.xL ? m : 99u;
         const uint32_t ciR = s63 ? B - 1u : (t == pc.xL + 1u ? m : 99u);
-        // the ancestors (index >= 1; index 0 is the new slot itself)
-        const uint64_t cL = (ciL - 1u) < 7u ? L : ~0ull, cR = (ciR - 1u) < 7u ? R : ~0ull;
-        const uint32_t h = (uint32_t)(__builtin_popcountll(ballot(val > cL)) + __builtin_popcountll(ballot(val > cR)));
+        // the ancestors (index >= 1; index 0 is the new slot itself), as lane masks
+        const uint64_t aL = ballot((ciL - 1u) < 7u), aR = ballot((ciR - 1u) < 7u);
+        const uint32_t h = (uint32_t)(__builtin_popcountll(ballot(val > L) & aL) + __builtin_popcountll(ballot(val > R) & aR));
         const bool odd = in_mask(0xAAAAAAAAAAAAAAAAull); // father slot p odd: an L half
         const uint64_t f = odd ? fL : fR;
         const int32_t fI = odd ? fIL : fIR;
@@ -466,15 +465,12 @@ __device__ __forceinline__ void greedy_upper_inl(const SearchArgs &a, const floa
                 dk = ord32(pq_distance_code<true>(a, lut, v, c8));
             ndis += nvalid;
             nhops += 1;
-            // sequential `if (dis < d_nearest)` in link order == first lane holding the minimum
-            uint64_t key = (lane < nvalid) ? (((uint64_t)dk << 32) | (uint32_t)lane) : ~0ull;
-            key = wave_min_u64(key);
-            if (key != ~0ull) {
-                const uint32_t bk = (uint32_t)(key >> 32);
-                if (bk < dn) {
-                    dn = bk;
-                    nearest = __builtin_amdgcn_readlane(v, (int)(key & 63));
-                }
+            // sequential `if (dis < d_nearest)` in link order == the first lane holding the minimum: a DPP min over the
+            // wave, then the lowest lane equal to it (no 64-bit shuffle reduction)
+            const uint32_t mn = wave_min_u32(dk); // invalid lanes hold ~0, never below dn
+            if (mn < dn) {
+                dn = mn;
+                nearest = __builtin_amdgcn_readlane(v, __builtin_ctzll(ballot(dk == mn)));
             }
             if (nearest == prev)
                 break;

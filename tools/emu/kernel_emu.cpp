@@ -75,7 +75,7 @@ extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t
         u64 rem = jmax >= 64 ? ~0ull : ((1ull << jmax) - 1ull);
         auto below_root = [&]() { bool c[W]; for (int l = 0; l < W; ++l) c[l] = dall[l] < hi32(root); return ballot(c); };
         if (kc < ef) { // the heap fills
-            while (rem && kc < ef) {
+            while (rem) {
                 const int l = __builtin_ctzll(rem); rem &= rem - 1;
                 const u32 key = dall[l]; const int32_t idl = v1[l];
                 if (hp.holds(idl)) continue;
@@ -83,14 +83,13 @@ extern "C" int emu_search_one(const int32_t *nbr0, const uint8_t *codes, int64_t
                 hp.push_fill(kc, pack(key, idl), idl, pc);
                 ++nvalid;
                 pushed.push_back(idl);
+                if (kc == ef) { // the root is read once the heap is full (push_fill does not track it)
+                    root = hp.R[63]; rootI = hp.IR[63];
+                    break;
+                }
             }
-            if (kc == ef) { // the root is read once the heap is full (push_fill does not track it)
-                root = hp.R[63]; rootI = hp.IR[63];
-                rem &= below_root();
-            }
-        } else {
-            rem &= below_root();
         }
+        rem &= below_root();
         while (rem) { // the full heap: pop the max, push val; log an evicted entry tied with the new root
             const int l = __builtin_ctzll(rem); rem &= rem - 1;
             const u32 key = dall[l];
