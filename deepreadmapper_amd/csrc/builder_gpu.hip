@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hn
             break;
         }
         const int32_t u = a.order[a.start + qi];
-        build_lut_m8_ptr(a.x + (size_t)u * a.d, a.centroids, lut, lane);
+        build_lut_m8_ptr<1>(a.x + (size_t)u * a.d, a.centroids, lut, lane);
         const int ul = a.levels[u];
         int32_t cur = a.entry_point;
         uint32_t dcur = __builtin_amdgcn_readfirstlane(adc8(lut, a.codes, cur));

@@ -175,9 +175,13 @@ __device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float 
 
 // set_query for the lean kernel (M = 8, ksub = 256, dsub = 16, 16-B aligned queries): the same
 // per-entry op order as build_lut, with the query sub-vector made wave-uniform (SGPRs) so that only
-// the two centroids a lane works on occupy VGPRs (32 of them).
+// the centroids a lane works on occupy VGPRs. A lane sums 2 H entries of a sub-quantizer at once, their 8 H
+// centroid loads issued together: 16 / H load round trips per LUT. The search takes H = 2 (round 5: C5 search
+// 96.0 -> 95.6 ms, profiles/r05/ab_search_lut_unroll.txt); the builder keeps H = 1 (its 55 VGPRs would double).
+template <int H>
 __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *centroids, float *lut, int lane)
 {
+    typedef float f2 __attribute__((ext_vector_type(2)));
     for (int m = 0; m < 8; ++m) {
         float xs[16];
 #pragma unroll
@@ -189,24 +193,25 @@ __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *c
             xs[4 * i + 3] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t.w)));
         }
 #pragma unroll 1
-        for (int c0 = 0; c0 < 256; c0 += 128) {
-            const int e0 = m * 256 + c0 + lane;
-            const float4 *ca = reinterpret_cast<const float4 *>(centroids + (size_t)e0 * 16);
-            const float4 *cb = reinterpret_cast<const float4 *>(centroids + (size_t)(e0 + 64) * 16);
-            float4 u[4], w[4];
+        for (int c0 = 0; c0 < 256; c0 += 128 * H) {
+        const float4 *cq = reinterpret_cast<const float4 *>(centroids) + ((size_t)m * 256 + c0 + lane) * 4;
+        float4 u[H][4], w[H][4];
+#pragma unroll
+        for (int h = 0; h < H; ++h)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                u[i] = ca[i];
-                w[i] = cb[i];
+                u[h][i] = cq[h * 512 + i];
+                w[h][i] = cq[h * 512 + 256 + i];
             }
-            // the two entries' chains side by side in the halves of packed fp32 ops (v_pk_add_f32 / v_pk_mul_f32):
-            // each entry keeps its own sequence of IEEE round-to-nearest subtract, multiply, add (no contraction)
-            typedef float f2 __attribute__((ext_vector_type(2)));
+        // two entries' chains side by side in the halves of packed fp32 ops (v_pk_add_f32 / v_pk_mul_f32): each
+        // entry keeps its own sequence of IEEE round-to-nearest subtract, multiply, add (no contraction)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
             f2 acc = {0.0f, 0.0f};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float cu[4] = {u[i].x, u[i].y, u[i].z, u[i].w};
-                const float cw[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
+                const float cu[4] = {u[h][i].x, u[h][i].y, u[h][i].z, u[h][i].w};
+                const float cw[4] = {w[h][i].x, w[h][i].y, w[h][i].z, w[h][i].w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const f2 x2 = {xs[4 * i + j], xs[4 * i + j]};
@@ -215,15 +220,17 @@ __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *c
                     acc = acc + d * d;
                 }
             }
+            const int e0 = m * 256 + c0 + h * 128 + lane;
             lut[e0] = acc.x;
             lut[e0 + 64] = acc.y;
+        }
         }
     }
     __syncthreads();
 }
 __device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, float *lut, int lane)
 {
-    build_lut_m8_ptr(a.x + q * a.d, a.centroids, lut, lane);
+    build_lut_m8_ptr<2>(a.x + q * a.d, a.centroids, lut, lane);
 }
 
 // greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss]

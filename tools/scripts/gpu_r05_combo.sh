@@ -14,4 +14,4 @@ if [ ${#W[@]} -gt 0 ]; then
   bash tools/scripts/ab_sw.sh "${W[@]}" > gpurun_out/ab_sw_$TAG.txt 2>&1 || { echo AB_SW_FAILED; tail -5 gpurun_out/ab_sw_$TAG.txt; exit 1; }
   cat gpurun_out/ab_sw_$TAG.txt
 fi
-[ "${FULL:-1}" = "1" ] && TAG=$TAG bash tools/scripts/gpu_r05_full.sh
+if [ "${FULL:-1}" = "1" ]; then TAG=$TAG bash tools/scripts/gpu_r05_full.sh; fi
