@@ -542,6 +542,40 @@ def run_c4(args, D):
     D.close()
 
 
+def sw_band_timing(table, d_I, d_q, d_ql, qstride, Q, K, band, search_ms, sw_ms, ids_full, sc_full, truth, stream):
+    """The opt-in banded SW rerank (an extension; the reference scores the full DP) on the timed step's search rows:
+    its time, the step it would make, and how far its results move from the full DP's (NOT the headline)."""
+    from deepreadmapper_amd.device import DeviceBuffer, Event
+    from deepreadmapper_amd._native import check, lib
+    d_sc, d_id, d_st = DeviceBuffer((Q, K), np.int32), DeviceBuffer((Q, K), np.uint64), DeviceBuffer(Q, np.int32)
+
+    def run():
+        check(lib().drm_post_process_sw_static_device(table.handle, d_I.ptr, Q, K, d_q.ptr, d_ql.ptr, qstride, 1, K, K,
+                                                      d_sc.ptr, d_id.ptr, d_st.ptr, stream.handle))
+    table.sw_band = band
+    try:
+        run()
+        ts = []
+        for _ in range(3):
+            e0, e1 = Event(), Event()
+            e0.record(stream)
+            run()
+            e1.record(stream)
+            stream.synchronize()
+            ts.append(e0.elapsed_ms(e1))
+    finally:
+        table.sw_band = 0
+    ms = float(np.mean(ts))
+    ids, sc = d_id.download(), d_sc.download()
+    return {"band": band, "note": "opt-in banded DP (cells |i - j| <= band), not parity with the reference; the "
+                                  "headline above is the full DP",
+            "sw_rerank_ms": round(ms, 3), "full_dp_sw_rerank_ms": round(sw_ms, 3),
+            "step_ms": round(search_ms + ms, 3), "reads_per_s_device": round(Q / ((search_ms + ms) * 1e-3), 1),
+            "top1_id_equal_full": round(float(np.mean(ids[:, 0] == ids_full[:, 0])), 4),
+            "topk_scores_equal_full": round(float(np.mean(sc == sc_full)), 4),
+            "truth_top1": round(float(np.mean(ids[:, 0].astype(np.int64) == truth)), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -563,6 +597,9 @@ def main():
     ap.add_argument("--index", choices=["pq", "flat"], default="pq",
                     help="pq (default): faiss IndexHNSWPQ, the live pipeline's index (src/main.cpp:236-237); flat: "
                          "hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib defaults) over the C3 windows")
+    ap.add_argument("--sw-band", type=int, default=0, choices=[0, 8, 16, 32],
+                    help="also time the opt-in banded SW rerank (drm_refs_set_sw_band, NOT parity with the reference) on "
+                         "the same search rows, reported beside the headline as `sw_band_opt_in`; 0 = skip")
     ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c5",
                     help="c5 (default): the metric's configuration (50M windows, 1.25M reads per GPU), search + SW "
                          "rerank; c3: 1M windows, 100k reads per GPU, search + SW rerank; c4: search only on a 10M-vector "
@@ -745,6 +782,9 @@ def main():
     l2 = None if (args.no_l2 or flat) else l2_timing(table, d_I, d_x, d_q, queries.shape[1], args.embed == "gru", Q, K,
                                                          truth, dev)
 
+    band = sw_band_timing(table, d_I, d_q, d_ql, queries.shape[1], Q, K, args.sw_band, search_ms, sw_ms, ids,
+                          d_sc.download(), truth, stream) if (args.sw_band and not flat) else None
+
     total_reads = float(N * Q * args.steps)
     value = total_reads / elapsed_max
     gather = gather_results(D, dev, N * Q, [("sw_ids", d_id), ("sw_scores", d_sc), ("search_ids", d_L if flat else d_I),
@@ -812,6 +852,7 @@ def main():
             "encoder": dict(enc, with_search_rerank_reads_per_s=round(Q / ((elapsed_max / args.steps) + enc["ms"] * 1e-3), 1))
             if enc else None,
             "l2_rerank": l2,
+            "sw_band_opt_in": band,
             "breakdown": {"schedule": "sequential: search, then SW rerank, each with the whole chip",
                           "device_span_ms": round(span_ms, 3),
                           "search_ms": round(search_ms, 3), "sw_rerank_ms": round(sw_ms, 3),

@@ -35,6 +35,7 @@ EXPORTS = [
     "drm_refs_get_info", "drm_host_alloc", "drm_host_free", "drm_search_rerank", "drm_multi_create",
     "drm_multi_free", "drm_multi_get_index_info", "drm_multi_search_rerank", "drm_comm_unique_id", "drm_comm_init",
     "drm_comm_free", "drm_comm_gather_rows", "drm_refs_create_genome", "drm_refs_is_genome",
+    "drm_refs_set_sw_band", "drm_refs_get_sw_band",
     "drm_extract_fasta_sequence", "drm_post_process_sw_dynamic", "drm_post_process_sw_dynamic_device",
     "drm_multi_create_genome", "drm_search_rerank_prepare",
     "drm_encoder_load", "drm_encoder_export", "drm_encoder_free", "drm_encoder_get_info", "drm_tokenize",
@@ -162,6 +163,8 @@ def lib():
         "drm_comm_gather_rows": (C.c_int, [vp, vp, i64, i64, vp, C.c_int, vp]),
         "drm_refs_create_genome": (C.c_int, [vp, i64, i32, C.c_int, C.POINTER(vp)]),
         "drm_refs_is_genome": (C.c_int, [vp, C.POINTER(C.c_int)]),
+        "drm_refs_set_sw_band": (C.c_int, [vp, i32]),
+        "drm_refs_get_sw_band": (C.c_int, [vp, C.POINTER(i32)]),
         "drm_multi_create_genome": (C.c_int, [C.c_char_p, vp, C.c_int, vp, i64, i32, C.POINTER(vp)]),
         "drm_search_rerank_prepare": (C.c_int, [vp, i64, i32, i32, i32, i32]),
         "drm_extract_fasta_sequence": (C.c_int, [C.c_char_p, vp, C.POINTER(i64)]),

@@ -808,6 +808,23 @@ int drm_sw_scores(const uint8_t *s1, const int64_t *off1, const int32_t *len1, c
     });
 }
 
+namespace {
+// the opt-in banded SW (drm_refs_set_sw_band): 0 (full DP, the reference's) or 8 / 16 / 32
+void check_sw_band(int32_t band)
+{
+    if (band != 0 && band != 8 && band != 16 && band != 32)
+        throw Error(DRM_ERR_ARG, "SW band must be 0 (full DP), 8, 16 or 32, got " + std::to_string(band));
+}
+// the initial band of a new handle: DRM_SW_BAND (unset: 0), so that the pipeline CLI can opt in without new argv
+int32_t env_sw_band()
+{
+    const char *e = std::getenv("DRM_SW_BAND");
+    const int32_t band = e ? (int32_t)std::atoi(e) : 0;
+    check_sw_band(band);
+    return band;
+}
+} // namespace
+
 int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int64_t row_stride, int device,
                     drm_refs **out)
 {
@@ -819,6 +836,7 @@ int drm_refs_create(const uint8_t *windows, int64_t n_ref, int32_t ref_len, int6
         DRM_HIP_CHECK(hipSetDevice(device));
         std::unique_ptr<drm_refs> r(new drm_refs());
         r->dev.device = device;
+        r->dev.sw_band = env_sw_band();
         r->dev.n_ref = n_ref;
         r->dev.ref_len = ref_len;
         r->dev.row_stride = std::max<int64_t>(16, ((int64_t)ref_len + 15) / 16 * 16);
@@ -856,6 +874,7 @@ int drm_refs_create_genome(const uint8_t *genome, int64_t len, int32_t ref_len, 
         DRM_HIP_CHECK(hipSetDevice(device));
         std::unique_ptr<drm_refs> r(new drm_refs());
         r->dev.device = device;
+        r->dev.sw_band = env_sw_band();
         r->dev.ref_len = ref_len;
         r->dev.row_stride = 16;
         r->dev.glen = len;
@@ -887,6 +906,25 @@ int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, in
             *ref_len = refs->dev.ref_len;
         if (device)
             *device = refs->dev.device;
+    });
+}
+
+int drm_refs_set_sw_band(drm_refs *refs, int32_t band)
+{
+    return guarded([&] {
+        if (!refs)
+            throw Error(DRM_ERR_ARG, "null argument");
+        check_sw_band(band);
+        refs->dev.sw_band = band;
+    });
+}
+
+int drm_refs_get_sw_band(const drm_refs *refs, int32_t *band)
+{
+    return guarded([&] {
+        if (!refs || !band)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *band = refs->dev.sw_band;
     });
 }
 
@@ -1036,7 +1074,9 @@ static int post_process_host(bool dynamic, drm_refs *refs, const int64_t *neighb
         }
         if (first_over >= 0)
             throw Error(DRM_ERR_UNSUPPORTED, "query " + std::to_string(first_over) + " expands to more than " +
-                                                 std::to_string(drm::kMaxCands) + " candidates or exceeds the SW length limit");
+                                                 std::to_string(drm::kMaxCands) +
+                                                 " candidates or exceeds the SW kernels' limits (query length; banded: 256"
+                                                 " bytes, 7 distinct query bytes)");
         if (first_bad >= 0) {
             if (bad_query)
                 *bad_query = first_bad;

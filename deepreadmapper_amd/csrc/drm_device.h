@@ -231,6 +231,8 @@ struct DeviceRefs {
     float *emb = nullptr;
     int32_t emb_dim = 0;
     int64_t emb_rows = 0;
+    // opt-in banded SW (drm_refs_set_sw_band): 0 = the full DP of the reference (default), else the band half-width
+    int32_t sw_band = 0;
 };
 
 struct RerankArgs {

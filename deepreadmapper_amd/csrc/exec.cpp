@@ -255,7 +255,8 @@ void check_status(const int32_t *status, int64_t n, int32_t k)
     }
     if (first_over >= 0)
         throw Error(DRM_ERR_UNSUPPORTED, "query " + std::to_string(first_over) +
-                                             " expands to more than 1024 candidates or exceeds the SW length limit");
+                                             " expands to more than 1024 candidates or exceeds the SW kernels' limits (query"
+                                             " length; banded: 256 bytes, 7 distinct query bytes)");
     if (first_bad >= 0)
         throw Error(DRM_ERR_CANDS, "Not enough candidates (query " + std::to_string(first_bad) + ": fewer than " +
                                        std::to_string(k) + ")");

@@ -687,6 +687,209 @@ __global__ __launch_bounds__(64) void sw_score_f16_kernel(RerankArgs a)
     }
 }
 
+// ------------------------------------------------------------------------ banded DP (opt-in, non-parity)
+// The reference leaves banding as a TODO (includes/utils/reranker.hpp:12) and scores the full DP, so this is an
+// opt-in mode of this implementation (drm_refs_set_sw_band), never the default: the recurrence of metrics.cpp:30-41
+// restricted to the cells |i - j| <= W (row i over the candidate, column j over the query, both 0-based), a cell
+// outside the band being 0 (oracle_calc_sw_score_banded). The score is at most the full one and equal to it when the
+// best local alignment lies inside the band.
+//
+// Layout: one wave per query, two candidates per lane (16-bit halves, integer cells as in sw_rows_i16). The band of
+// row i is B = 2W + 1 registers, cell k holding column j = i - W + k, so a row's update is the full kernel's with
+// static indices: diag = the old cell k, up = the old cell k + 1 (0 past the band), left = the new cell k - 1. The
+// match terms come from a byte profile in LDS: per query byte code c (the query's distinct bytes, at most 7, plus an
+// 'absent' code that matches nothing) one byte per query position (2 on a match), padded by W zero positions on the
+// left, in 4 copies shifted by 0..3 bytes so that a row's band starts on a word boundary of copy i & 3. One v_perm
+// per cell pair takes candidate a's byte into the low half and candidate b's into the high half: 4.5 VALU per cell
+// pair. Positions left of the query (j < 0) are 0 in every row (the zero border); positions right of it match
+// nothing, and such cells never exceed a cell to their left, so the running best is unchanged (the same argument as
+// the padding of sw_score_kernel); rows past qlen + W - 1 hold only such cells and are skipped.
+constexpr int kBandQMax = 256; // longest query the banded kernel takes (longer: status -3, unsupported)
+constexpr int kBandCodes = 8;  // per query: up to 7 distinct query bytes + 'absent'
+
+__host__ __device__ constexpr int band_words(int w) { return (2 * w + 1 + 3) / 4; }
+
+template <int W>
+__global__ __launch_bounds__(64) void sw_score_band_kernel(RerankArgs a, int rsw)
+{
+    constexpr int B = 2 * W + 1;
+    constexpr int NWB = band_words(W);
+    __shared__ __align__(16) uint8_t qbuf[kBandQMax];
+    __shared__ uint8_t code_of[256];
+    __shared__ uint32_t qmask[8];
+    __shared__ int ncand_s;
+    extern __shared__ __align__(16) uint32_t band_lds[];
+    uint32_t *bprof = band_lds;                       // [4 copies][kBandCodes][rsw]
+    uint32_t *cand = band_lds + 4 * kBandCodes * rsw; // [a.cmax]
+    const int lane = threadIdx.x & 63;
+    for (int64_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+        const int qlen = a.q_len[q];
+        const int nsel = min(a.k_clusters, a.kk);
+        const int64_t *nb = a.neighbors + q * a.kk;
+        if (a.stride == 1 && nsel <= kMaxCands && !a.genome) {
+            // dense (post_processor.cpp:215-236): keep ids < n_ref, in order -- ballot compaction
+            int base = 0;
+            for (int c = 0; c < nsel; c += 64) {
+                const int i = c + lane;
+                const uint64_t id = (i < nsel) ? (uint64_t)nb[i] : ~0ull;
+                const bool keep = id < (uint64_t)a.n_ref;
+                const uint64_t m = __ballot(keep);
+                if (keep)
+                    cand[base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = (uint32_t)id;
+                base += __popcll(m);
+            }
+            if (lane == 0)
+                ncand_s = base;
+        } else if (lane == 0) {
+            ncand_s = find_candidates(a, nb, nsel, cand, a.cmax); // sparse or dynamic lookup
+        }
+        for (int t = lane; t < kBandQMax; t += 64)
+            qbuf[t] = t < qlen ? a.queries[q * a.q_stride + t] : 0;
+        if (lane < 8)
+            qmask[lane] = 0u;
+        __syncthreads();
+        for (int t = lane; t < qlen && t < kBandQMax; t += 64)
+            atomicOr(&qmask[qbuf[t] >> 5], 1u << (qbuf[t] & 31));
+        __syncthreads();
+        // byte codes: the query's distinct bytes in ascending order take 0, 1, ...; every other byte is 'absent'
+        int ndist = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            ndist += __popc(qmask[w]);
+        for (int b = lane; b < 256; b += 64) {
+            int rank = 0;
+            for (int w = 0; w < (b >> 5); ++w)
+                rank += __popc(qmask[w]);
+            const uint32_t m = qmask[b >> 5];
+            rank += __popc(m & ((1u << (b & 31)) - 1u));
+            const bool in_q = ((m >> (b & 31)) & 1u) != 0u;
+            code_of[b] = (uint8_t)(in_q && rank < kBandCodes - 1 ? rank : kBandCodes - 1);
+        }
+        __syncthreads();
+        // the byte profile: copy s, word x holds positions 4x + s .. 4x + s + 3 (query column position - W)
+        for (int it = lane; it < 4 * rsw; it += 64) {
+            const int s = it / rsw, x = it - s * rsw;
+            uint32_t cq = 0u; // the 4 positions' codes, 0xFF outside the query
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = 4 * x + e + s - W;
+                const uint32_t c = (j >= 0 && j < qlen) ? (uint32_t)code_of[qbuf[j]] : 0xFFu;
+                cq |= c << (8 * e);
+            }
+#pragma unroll
+            for (int c = 0; c < kBandCodes; ++c) {
+                uint32_t w = 0u;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    w |= ((cq >> (8 * e)) & 255u) == (uint32_t)c && c != kBandCodes - 1 ? 2u << (8 * e) : 0u;
+                bprof[(s * kBandCodes + c) * rsw + x] = w;
+            }
+        }
+        __syncthreads();
+        const bool unsupported = qlen > kBandQMax || ndist > kBandCodes - 1;
+        const int ncand = unsupported ? -3 : ncand_s;
+        const int L = a.ref_len;
+        const int rows = min(L, qlen + W); // later rows hold only cells right of the query
+        for (int c0 = lane; c0 < ncand; c0 += 128) {
+            const int c1 = c0 + 64;
+            const bool has_b = c1 < ncand;
+            uint32_t H[B];
+#pragma unroll
+            for (int k = 0; k < B; ++k)
+                H[k] = 0u;
+            uint32_t best = 0u;
+            const uint32_t wa = cand[c0], wb = has_b ? cand[c1] : cand[c0];
+            const CandRow ra(a, wa), rb(a, wb);
+            // static table: 16 candidate bytes per load (rows i .. i + 15), the next block in flight; dynamic lookup:
+            // one byte per row, one row ahead
+            const uint4 *pa = reinterpret_cast<const uint4 *>(a.refs + (size_t)wa * (size_t)a.row_stride);
+            const uint4 *pb = reinterpret_cast<const uint4 *>(a.refs + (size_t)wb * (size_t)a.row_stride);
+            const int nblk = (int)(a.row_stride >> 4);
+            uint4 ba = make_uint4(0u, 0u, 0u, 0u), bb = ba, na4 = ba, nb4 = ba;
+            uint32_t wa4 = 0u, wb4 = 0u;
+            int nca = -1, ncb = -1;
+            if (rows > 0) {
+                if (a.genome) {
+                    nca = ra.at(0);
+                    ncb = has_b ? rb.at(0) : -1;
+                } else {
+                    na4 = pa[0];
+                    nb4 = pb[0];
+                }
+            }
+            for (int i = 0; i < rows; ++i) {
+                int ca, cb;
+                if (a.genome) {
+                    ca = nca;
+                    cb = ncb;
+                    if (i + 1 < rows) {
+                        nca = ra.at(i + 1);
+                        ncb = has_b ? rb.at(i + 1) : -1;
+                    }
+                } else {
+                    if ((i & 3) == 0) {
+                        if ((i & 15) == 0) {
+                            ba = na4;
+                            bb = nb4;
+                            const int nx = (i >> 4) + 1;
+                            if (nx < nblk && 16 * nx < rows) {
+                                na4 = pa[nx];
+                                nb4 = pb[nx];
+                            }
+                        }
+                        wa4 = ba.x;
+                        wb4 = bb.x;
+                        ba = make_uint4(ba.y, ba.z, ba.w, 0u);
+                        bb = make_uint4(bb.y, bb.z, bb.w, 0u);
+                    }
+                    const uint32_t sh = 8u * (uint32_t)(i & 3);
+                    ca = (int)((wa4 >> sh) & 255u);
+                    cb = has_b ? (int)((wb4 >> sh) & 255u) : -1;
+                }
+                const int ka = ca < 0 ? kBandCodes - 1 : (int)code_of[ca];
+                const int kb = cb < 0 ? kBandCodes - 1 : (int)code_of[cb];
+                // the band of row i starts at padded position i: copy i & 3, word i >> 2
+                const uint32_t *qa = bprof + ((i & 3) * kBandCodes + ka) * rsw + (i >> 2);
+                const uint32_t *qb = bprof + ((i & 3) * kBandCodes + kb) * rsw + (i >> 2);
+                uint32_t xa[NWB], xb[NWB];
+#pragma unroll
+                for (int n = 0; n < NWB; ++n) {
+                    xa[n] = qa[n];
+                    xb[n] = qb[n];
+                }
+                uint32_t left = 0u, prev = 0u;
+#pragma unroll
+                for (int k = 0; k < B; ++k) {
+                    const uint32_t e = (uint32_t)(k & 3);
+                    // bytes: [a's term, 0, b's term, 0]
+                    const uint32_t term = __builtin_amdgcn_perm(xb[k >> 2], xa[k >> 2], 0x0C000C00u | ((4u + e) << 16) | e);
+                    const uint32_t t = H[k] + term;
+                    const uint32_t up = k + 1 < B ? H[k + 1] : 0u;
+                    const uint32_t h = idec(imax3(t, up, left));
+                    H[k] = h;
+                    left = h;
+                    if (k & 1)
+                        best = imax3(best, prev, h);
+                    else if (k == B - 1)
+                        best = imax3(best, h, h);
+                    prev = h;
+                }
+            }
+            const bool dense_dyn = a.genome && a.stride == 1; // the search's own id (post_processor.cpp:95-101)
+            a.cand_ids[q * a.cmax + c0] = dense_dyn ? (uint64_t)nb[c0] : wa;
+            a.cand_scores[q * a.cmax + c0] = (int)(best & 0xFFFFu);
+            if (has_b) {
+                a.cand_ids[q * a.cmax + c1] = dense_dyn ? (uint64_t)nb[c1] : wb;
+                a.cand_scores[q * a.cmax + c1] = (int)(best >> 16);
+            }
+        }
+        __syncthreads();
+        if (lane == 0)
+            a.ncand[q] = ncand;
+        __syncthreads();
+    }
+}
+
 // Kernel 2 of the rerank: sw_reranker's std::partial_sort + output, one thread per query. Each
 // thread replays libstdc++'s heap algorithm on its own padded LDS array (stride: an odd number of words, so
 // threads touching the same heap index hit different banks). The block loads its queries' score rows and writes
@@ -832,6 +1035,26 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     const size_t cand_lds = sizeof(uint32_t) * (size_t)cmax; // sw_score_f16_kernel's candidate list
     // fp16 pair-profile kernel for queries up to 152 bytes; the bit-profile kernel re-scores the
     // queries it flagged, and takes longer queries (or everything when DRM_SW_BITPROFILE=1).
+    if (refs.sw_band > 0) {
+        // opt-in banded DP (non-parity): one kernel for every query (status -3 past its limits)
+        const int W = refs.sw_band;
+        const int qm = std::max(1, std::min(max_qlen, kBandQMax));
+        const int rsw = (((qm + W - 1) >> 2) + band_words(W)) | 1; // odd: the copies' rows spread over the banks
+        const size_t lds = sizeof(uint32_t) * ((size_t)4 * kBandCodes * (size_t)rsw + (size_t)cmax);
+        switch (W) {
+        case 8:
+            hipLaunchKernelGGL((sw_score_band_kernel<8>), dim3(grid_f16), dim3(64), lds, stream, a, rsw);
+            break;
+        case 16:
+            hipLaunchKernelGGL((sw_score_band_kernel<16>), dim3(grid_f16), dim3(64), lds, stream, a, rsw);
+            break;
+        case 32:
+            hipLaunchKernelGGL((sw_score_band_kernel<32>), dim3(grid_f16), dim3(64), lds, stream, a, rsw);
+            break;
+        default:
+            throw Error(DRM_ERR_ARG, "SW band must be 8, 16 or 32");
+        }
+    } else {
     static const bool force_bits = [] {
         const char *e = std::getenv("DRM_SW_BITPROFILE");
         return e && std::atoi(e) != 0;
@@ -858,6 +1081,7 @@ void launch_sw_rerank(DeviceRefs &refs, RerankArgs a, int max_qlen, hipStream_t 
     default:
         hipLaunchKernelGGL((sw_score_kernel<256>), dim3(grid), dim3(64), 0, stream, a);
         break;
+    }
     }
     DRM_HIP_CHECK(hipGetLastError());
     // 16-bit elements when every score (<= the window length) and every candidate index fits a byte: half the LDS

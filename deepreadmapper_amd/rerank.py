@@ -36,7 +36,22 @@ def calc_sw_score(seq1, seq2):
     return int(calc_sw_scores([seq1], [seq2])[0])
 
 
-class WindowTable:
+class _SwBand:
+    """The opt-in banded SW of a window / genome handle (drm_refs_set_sw_band): 0 = the reference's full DP
+    (default, bit-exact); 8, 16 or 32 = only the cells |i - j| <= band (non-parity, see include/drm_hip.h)."""
+
+    @property
+    def sw_band(self):
+        b = C.c_int32(0)
+        check(lib().drm_refs_get_sw_band(self._h, C.byref(b)))
+        return b.value
+
+    @sw_band.setter
+    def sw_band(self, band):
+        check(lib().drm_refs_set_sw_band(self._h, int(band)))
+
+
+class WindowTable(_SwBand):
     """Device-resident `ref_seqs` (static lookup table of equal-length windows)."""
 
     def __init__(self, windows, device=0):
@@ -71,7 +86,7 @@ class WindowTable:
             pass
 
 
-class GenomeTable:
+class GenomeTable(_SwBand):
     """Device-resident genome string for the dynamic lookup (use_dynamic): window id w is
     genome[w // 2 : w // 2 + ref_len], reverse-complemented when w is odd (find_sequence,
     src/utils/post_processor.cpp:47-64)."""

@@ -200,6 +200,15 @@ int drm_refs_is_genome(const drm_refs *refs, int *is_genome);
 int drm_extract_fasta_sequence(const char *path, uint8_t *out, int64_t *len);
 /* Shape and device of a window table (any out-pointer may be NULL). */
 int drm_refs_get_info(const drm_refs *refs, int64_t *n_ref, int32_t *ref_len, int *device);
+/* Opt-in banded Smith-Waterman for every rerank on this handle (an extension: the reference scores the full DP and
+ * leaves banding as a TODO, includes/utils/reranker.hpp:12). band 0 = the full DP, bit-exact with calc_sw_score
+ * (the default); band 8, 16 or 32 = only the cells with |i - j| <= band (row i over the window, column j over the
+ * query, both 0-based), a cell outside the band being 0: the score is at most the full one and equal to it when the
+ * best local alignment stays inside the band (NOT parity with the reference). Other values: DRM_ERR_ARG. A new handle
+ * starts at $DRM_SW_BAND (unset: 0). Banded queries are limited to 256 bytes and 7 distinct byte values (otherwise
+ * the rerank fails with DRM_ERR_UNSUPPORTED). */
+int drm_refs_set_sw_band(drm_refs *refs, int32_t band);
+int drm_refs_get_sw_band(const drm_refs *refs, int32_t *band);
 
 /* post_process_sw_static (src/utils/post_processor.cpp:454-549) -> find_sequences (static,
  * :204-336) -> sw_reranker (src/utils/reranker.cpp:3-51) -> calc_sw_score, for nq queries.

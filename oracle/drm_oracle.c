@@ -57,6 +57,39 @@ int oracle_calc_sw_score(const uint8_t *s1, int64_t len1, const uint8_t *s2, int
 }
 
 /* ========================================================================================
+ * Banded Smith-Waterman: an opt-in, NON-PARITY mode of this implementation (the reference has only
+ * a TODO for it, includes/utils/reranker.hpp:12). The recurrence of calc_sw_score restricted to
+ * the cells with |i - j| <= band (1-based row i over s1, column j over s2); a cell outside the
+ * band is 0, so an alignment path stays inside it. band <= 0 is the full DP above. The score is
+ * at most the full one and equals it when the best local alignment lies inside the band.
+ * ====================================================================================== */
+int oracle_calc_sw_score_banded(const uint8_t *s1, int64_t len1, const uint8_t *s2, int64_t len2, int64_t band)
+{
+    if (band <= 0)
+        return oracle_calc_sw_score(s1, len1, s2, len2);
+    if (len1 <= 0 || len2 <= 0)
+        return 0;
+    int *row = (int *)calloc((size_t)(len2 + 1), sizeof(int)); /* dp[i-1][*]; out-of-band cells hold 0 */
+    int best = 0;
+    for (int64_t i = 1; i <= len1; ++i) {
+        const uint8_t c1 = s1[i - 1];
+        int diag = 0, left = 0;
+        for (int64_t j = 1; j <= len2; ++j) {
+            const int up = row[j];
+            int h = 0;
+            if (j - i <= band && i - j <= band)
+                h = imax(imax(0, diag + (c1 == s2[j - 1] ? 1 : -1)), imax(up - 1, left - 1));
+            diag = up;
+            row[j] = h;
+            left = h;
+            best = imax(best, h);
+        }
+    }
+    free(row);
+    return best;
+}
+
+/* ========================================================================================
  * libstdc++ std::partial_sort with comp(a, b) := scores[a] > scores[b], the exact call of
  * src/utils/reranker.cpp:38-40. Restates __partial_sort = __heap_select + __sort_heap and the
  * helpers __make_heap / __adjust_heap / __push_heap / __pop_heap (bits/stl_heap.h,
@@ -135,7 +168,7 @@ void oracle_partial_sort_desc(int64_t *idx, int64_t n, int64_t k, const int32_t 
  * ====================================================================================== */
 static int64_t pp_one_query(const int64_t *nb, int64_t kk, const uint8_t *refs, int64_t n_ref, int64_t ref_len,
                             int64_t ref_stride, const uint8_t *q, int32_t qlen, int64_t stride, int64_t k,
-                            int64_t k_clusters, int32_t *out_scores, uint64_t *out_ids)
+                            int64_t k_clusters, int64_t band, int32_t *out_scores, uint64_t *out_ids)
 {
     /* :494-495  first min(k_clusters, n_i) neighbour ids, converted long -> size_t (:339-355) */
     const int64_t nsel = k_clusters < kk ? k_clusters : kk;
@@ -170,7 +203,7 @@ static int64_t pp_one_query(const int64_t *nb, int64_t kk, const uint8_t *refs, 
     }
     int32_t *scores = (int32_t *)malloc(sizeof(int32_t) * (size_t)ncand);
     for (int64_t c = 0; c < ncand; ++c)
-        scores[c] = oracle_calc_sw_score(refs + cand[c] * (uint64_t)ref_stride, ref_len, q, qlen);
+        scores[c] = oracle_calc_sw_score_banded(refs + cand[c] * (uint64_t)ref_stride, ref_len, q, qlen, band);
     if (ncand < k) { /* reranker.cpp:26-29 */
         free(scores);
         free(cand);
@@ -190,11 +223,11 @@ static int64_t pp_one_query(const int64_t *nb, int64_t kk, const uint8_t *refs, 
     return k;
 }
 
-int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *refs,
-                                      int64_t n_ref, int64_t ref_len, int64_t ref_stride, const uint8_t *queries,
-                                      const int32_t *q_len, int64_t q_stride, int64_t stride, int64_t k,
-                                      int64_t k_clusters, int nthreads, int32_t *top_scores, uint64_t *top_ids,
-                                      int32_t *counts)
+int64_t oracle_post_process_sw_static_banded(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *refs,
+                                             int64_t n_ref, int64_t ref_len, int64_t ref_stride, const uint8_t *queries,
+                                             const int32_t *q_len, int64_t q_stride, int64_t stride, int64_t k,
+                                             int64_t k_clusters, int64_t band, int nthreads, int32_t *top_scores,
+                                             uint64_t *top_ids, int32_t *counts)
 {
     if (k > k_clusters * 2 * stride) /* :486-489 */
         return -1000000000;
@@ -210,7 +243,7 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
             top_ids[i * k + j] = UINT64_MAX;
         }
         int64_t r = pp_one_query(neighbors + i * kk, kk, refs, n_ref, ref_len, ref_stride, queries + i * q_stride,
-                                 q_len[i], stride, k, k_clusters, top_scores + i * k, top_ids + i * k);
+                                 q_len[i], stride, k, k_clusters, band, top_scores + i * k, top_ids + i * k);
         counts[i] = r < 0 ? 0 : (int32_t)r;
         if (r < 0) {
 #ifdef _OPENMP
@@ -223,6 +256,17 @@ int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int6
         }
     }
     return first_bad >= 0 ? -(1 + first_bad) : 0;
+}
+
+int64_t oracle_post_process_sw_static(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *refs,
+                                      int64_t n_ref, int64_t ref_len, int64_t ref_stride, const uint8_t *queries,
+                                      const int32_t *q_len, int64_t q_stride, int64_t stride, int64_t k,
+                                      int64_t k_clusters, int nthreads, int32_t *top_scores, uint64_t *top_ids,
+                                      int32_t *counts)
+{
+    return oracle_post_process_sw_static_banded(neighbors, nq, kk, refs, n_ref, ref_len, ref_stride, queries, q_len,
+                                                q_stride, stride, k, k_clusters, 0, nthreads, top_scores, top_ids,
+                                                counts);
 }
 
 /* ========================================================================================
@@ -263,7 +307,7 @@ static int64_t find_sequence_dyn(const uint8_t *g, int64_t glen, uint64_t id, in
 
 static int64_t ppd_one_query(const int64_t *nb, int64_t kk, const uint8_t *g, int64_t glen, int64_t ref_len,
                              const uint8_t *q, int32_t qlen, int64_t stride, int64_t k, int64_t k_clusters,
-                             int32_t *out_scores, uint64_t *out_ids)
+                             int64_t band, int32_t *out_scores, uint64_t *out_ids)
 {
     const int64_t nsel = k_clusters < kk ? k_clusters : kk;
     int64_t cap = (stride == 1) ? (nsel > 0 ? nsel : 1) : (nsel * (2 * stride) + 1);
@@ -293,7 +337,7 @@ static int64_t ppd_one_query(const int64_t *nb, int64_t kk, const uint8_t *g, in
     uint8_t *buf = (uint8_t *)malloc((size_t)(ref_len > 0 ? ref_len : 1));
     for (int64_t c = 0; c < ncand; ++c) {
         const int64_t len = find_sequence_dyn(g, glen, cand[c], ref_len, buf);
-        scores[c] = oracle_calc_sw_score(buf, len, q, qlen);
+        scores[c] = oracle_calc_sw_score_banded(buf, len, q, qlen, band);
     }
     free(buf);
     if (ncand < k) {
@@ -315,10 +359,11 @@ static int64_t ppd_one_query(const int64_t *nb, int64_t kk, const uint8_t *g, in
     return k;
 }
 
-int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *genome,
-                                       int64_t glen, int64_t ref_len, const uint8_t *queries, const int32_t *q_len,
-                                       int64_t q_stride, int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
-                                       int32_t *top_scores, uint64_t *top_ids, int32_t *counts)
+int64_t oracle_post_process_sw_dynamic_banded(const int64_t *neighbors, int64_t nq, int64_t kk,
+                                              const uint8_t *genome, int64_t glen, int64_t ref_len,
+                                              const uint8_t *queries, const int32_t *q_len, int64_t q_stride,
+                                              int64_t stride, int64_t k, int64_t k_clusters, int64_t band,
+                                              int nthreads, int32_t *top_scores, uint64_t *top_ids, int32_t *counts)
 {
     if (k > k_clusters * 2 * stride) /* :390-393 */
         return -1000000000;
@@ -334,7 +379,7 @@ int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int
             top_ids[i * k + j] = UINT64_MAX;
         }
         int64_t r = ppd_one_query(neighbors + i * kk, kk, genome, glen, ref_len, queries + i * q_stride, q_len[i],
-                                  stride, k, k_clusters, top_scores + i * k, top_ids + i * k);
+                                  stride, k, k_clusters, band, top_scores + i * k, top_ids + i * k);
         counts[i] = r < 0 ? 0 : (int32_t)r;
         if (r < 0) {
 #ifdef _OPENMP
@@ -347,6 +392,15 @@ int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int
         }
     }
     return first_bad >= 0 ? -(1 + first_bad) : 0;
+}
+
+int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *genome,
+                                       int64_t glen, int64_t ref_len, const uint8_t *queries, const int32_t *q_len,
+                                       int64_t q_stride, int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
+                                       int32_t *top_scores, uint64_t *top_ids, int32_t *counts)
+{
+    return oracle_post_process_sw_dynamic_banded(neighbors, nq, kk, genome, glen, ref_len, queries, q_len, q_stride,
+                                                 stride, k, k_clusters, 0, nthreads, top_scores, top_ids, counts);
 }
 
 /* ========================================================================================

@@ -22,6 +22,10 @@ extern "C" {
 /* ---- Smith-Waterman (src/utils/metrics.cpp:10-45) ---- */
 int oracle_calc_sw_score(const uint8_t *seq1, int64_t len1, const uint8_t *seq2, int64_t len2);
 
+/* Banded SW (an opt-in, non-parity mode of this implementation; the reference has only a TODO,
+ * includes/utils/reranker.hpp:12): cells with |i - j| <= band, 0 outside; band <= 0 = full DP. */
+int oracle_calc_sw_score_banded(const uint8_t *seq1, int64_t len1, const uint8_t *seq2, int64_t len2, int64_t band);
+
 /* libstdc++ std::partial_sort(idx, idx+k, idx+n, [](a,b){return scores[a] > scores[b];})
  * (src/utils/reranker.cpp:35-40). idx must hold the iota sequence on entry. */
 void oracle_partial_sort_desc(int64_t *idx, int64_t n, int64_t k, const int32_t *scores);
@@ -46,6 +50,18 @@ int64_t oracle_post_process_sw_dynamic(const int64_t *neighbors, int64_t nq, int
                                        int64_t glen, int64_t ref_len, const uint8_t *queries, const int32_t *q_len,
                                        int64_t q_stride, int64_t stride, int64_t k, int64_t k_clusters, int nthreads,
                                        int32_t *top_scores, uint64_t *top_ids, int32_t *counts);
+
+/* the same two with the banded SW score (band <= 0: identical to the full ones) */
+int64_t oracle_post_process_sw_static_banded(const int64_t *neighbors, int64_t nq, int64_t kk, const uint8_t *refs,
+                                             int64_t n_ref, int64_t ref_len, int64_t ref_stride, const uint8_t *queries,
+                                             const int32_t *q_len, int64_t q_stride, int64_t stride, int64_t k,
+                                             int64_t k_clusters, int64_t band, int nthreads, int32_t *top_scores,
+                                             uint64_t *top_ids, int32_t *counts);
+int64_t oracle_post_process_sw_dynamic_banded(const int64_t *neighbors, int64_t nq, int64_t kk,
+                                              const uint8_t *genome, int64_t glen, int64_t ref_len,
+                                              const uint8_t *queries, const int32_t *q_len, int64_t q_stride,
+                                              int64_t stride, int64_t k, int64_t k_clusters, int64_t band,
+                                              int nthreads, int32_t *top_scores, uint64_t *top_ids, int32_t *counts);
 
 /* ---- faiss IndexHNSWPQ (upstream semantics, see DESIGN.md "oracle") ---- */
 typedef struct {

@@ -25,6 +25,10 @@ def lib():
         _lib.oracle_partial_sort_desc.restype = None
         _lib.oracle_post_process_sw_static.restype = C.c_int64
         _lib.oracle_post_process_sw_dynamic.restype = C.c_int64
+        _lib.oracle_calc_sw_score_banded.restype = C.c_int
+        _lib.oracle_calc_sw_score_banded.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int64]
+        _lib.oracle_post_process_sw_static_banded.restype = C.c_int64
+        _lib.oracle_post_process_sw_dynamic_banded.restype = C.c_int64
         _lib.oracle_hnswpq_search.restype = C.c_int
         _lib.oracle_pq_distance_table.restype = None
         _lib.oracle_calc_l2_dist.restype = C.c_float
@@ -64,6 +68,11 @@ def calc_sw_score(a: bytes, b: bytes) -> int:
     return lib().oracle_calc_sw_score(a, len(a), b, len(b))
 
 
+def calc_sw_score_banded(a: bytes, b: bytes, band: int) -> int:
+    """Banded SW (opt-in, non-parity; drm_oracle.c oracle_calc_sw_score_banded): cells |i - j| <= band."""
+    return lib().oracle_calc_sw_score_banded(a, len(a), b, len(b), band)
+
+
 def ref_calc_sw_score(a: bytes, b: bytes) -> int:
     return ref().ref_calc_sw_score(a, len(a), b, len(b))
 
@@ -82,8 +91,9 @@ def stl_partial_sort_desc(scores, k):
     return idx[:k]
 
 
-def post_process_sw_static(neighbors, refs, ref_len, queries, q_len, stride, k, k_clusters, nthreads=0):
-    """neighbors [nq, kk] int64; refs [n_ref, ref_stride] uint8; queries [nq, q_stride] uint8."""
+def post_process_sw_static(neighbors, refs, ref_len, queries, q_len, stride, k, k_clusters, nthreads=0, band=0):
+    """neighbors [nq, kk] int64; refs [n_ref, ref_stride] uint8; queries [nq, q_stride] uint8.
+    band > 0: the banded SW score (opt-in, non-parity) instead of calc_sw_score."""
     neighbors = np.ascontiguousarray(neighbors, dtype=np.int64)
     refs = np.ascontiguousarray(refs, dtype=np.uint8)
     queries = np.ascontiguousarray(queries, dtype=np.uint8)
@@ -92,16 +102,16 @@ def post_process_sw_static(neighbors, refs, ref_len, queries, q_len, stride, k, 
     scores = np.zeros((nq, k), dtype=np.int32)
     ids = np.zeros((nq, k), dtype=np.uint64)
     counts = np.zeros(nq, dtype=np.int32)
-    rc = lib().oracle_post_process_sw_static(
+    rc = lib().oracle_post_process_sw_static_banded(
         _p(neighbors, C.c_int64), C.c_int64(nq), C.c_int64(kk),
         _p(refs, C.c_uint8), C.c_int64(refs.shape[0]), C.c_int64(ref_len), C.c_int64(refs.shape[1]),
         _p(queries, C.c_uint8), _p(q_len, C.c_int32), C.c_int64(queries.shape[1]),
-        C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int(nthreads),
+        C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int64(band), C.c_int(nthreads),
         _p(scores, C.c_int32), _p(ids, C.c_uint64), _p(counts, C.c_int32))
     return int(rc), scores, ids, counts
 
 
-def post_process_sw_dynamic(neighbors, genome, ref_len, queries, q_len, stride, k, k_clusters, nthreads=0):
+def post_process_sw_dynamic(neighbors, genome, ref_len, queries, q_len, stride, k, k_clusters, nthreads=0, band=0):
     """post_process_sw_dynamic: neighbors [nq, kk] int64; genome uint8 (extract_FASTA_sequence);
     queries [nq, q_stride] uint8."""
     neighbors = np.ascontiguousarray(neighbors, dtype=np.int64)
@@ -112,10 +122,10 @@ def post_process_sw_dynamic(neighbors, genome, ref_len, queries, q_len, stride, 
     scores = np.zeros((nq, k), dtype=np.int32)
     ids = np.zeros((nq, k), dtype=np.uint64)
     counts = np.zeros(nq, dtype=np.int32)
-    rc = lib().oracle_post_process_sw_dynamic(
+    rc = lib().oracle_post_process_sw_dynamic_banded(
         _p(neighbors, C.c_int64), C.c_int64(nq), C.c_int64(kk), _p(genome, C.c_uint8), C.c_int64(genome.size),
         C.c_int64(ref_len), _p(queries, C.c_uint8), _p(q_len, C.c_int32), C.c_int64(queries.shape[1]),
-        C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int(nthreads),
+        C.c_int64(stride), C.c_int64(k), C.c_int64(k_clusters), C.c_int64(band), C.c_int(nthreads),
         _p(scores, C.c_int32), _p(ids, C.c_uint64), _p(counts, C.c_int32))
     return int(rc), scores, ids, counts
 

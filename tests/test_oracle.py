@@ -37,6 +37,31 @@ def test_oracle_vs_reference_build_random():
         assert O.calc_sw_score(a, b) == O.ref_calc_sw_score(a, b)
 
 
+def _banded_literal(a, b, band):
+    """The banded recurrence written out on the full matrix (the oracle's banded mode is an extension of this
+    implementation, not the reference's: metrics.cpp:30-41 on the cells |i - j| <= band, 0 outside)."""
+    H = np.zeros((len(a) + 1, len(b) + 1), dtype=np.int64)
+    for i in range(1, len(a) + 1):
+        for j in range(max(1, i - band), min(len(b), i + band) + 1):
+            H[i, j] = max(0, H[i - 1, j - 1] + (1 if a[i - 1] == b[j - 1] else -1), H[i - 1, j] - 1, H[i, j - 1] - 1)
+    return int(H.max())
+
+
+def test_banded_oracle_vs_literal():
+    """oracle_calc_sw_score_banded against the literal banded matrix; band 0 and any band covering both strings are
+    the full calc_sw_score, and a band never scores above the full DP."""
+    rng = np.random.default_rng(9)
+    for t in range(120):
+        a = bytes(rng.choice(list(b"ACGTN"), size=int(rng.integers(0, 60))).astype(np.uint8))
+        b = bytes(rng.choice(list(b"ACGT<>"), size=int(rng.integers(0, 60))).astype(np.uint8))
+        band = int(rng.choice([1, 2, 3, 8, 16, 32]))
+        got = O.calc_sw_score_banded(a, b, band)
+        assert got == _banded_literal(a, b, band), (a, b, band)
+        full = O.calc_sw_score(a, b)
+        assert got <= full and O.calc_sw_score_banded(a, b, 0) == full
+        assert O.calc_sw_score_banded(a, b, max(len(a), len(b)) + 1) == full
+
+
 def test_c1_score_matrix_sample():
     mat = np.load(os.path.join(GOLDEN, "sw_c1_matrix.npy"))
     ref = [l.strip() for l in open(os.path.join(GOLDEN, "test_data_ref.txt"), "rb") if l.strip()]

@@ -16,11 +16,13 @@ from deepreadmapper_amd.device import DeviceBuffer, Event, Stream  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--queries", type=int, default=200_000)
 ap.add_argument("--windows", type=int, default=1_000_000)
+ap.add_argument("--band", type=int, default=0, help="opt-in banded DP half-width (drm_refs_set_sw_band), 0 = full")
 a = ap.parse_args()
 K = 128
 g = synth.genome(a.windows // 2 + 149, seed=3)
 refs = synth.windows_lookup(g, 150, 1)
 table = WindowTable(refs)
+table.sw_band = a.band
 rng = np.random.default_rng(1)
 I = rng.integers(0, len(refs), size=(a.queries, K)).astype(np.int64)
 d_I = DeviceBuffer.from_host(I)
@@ -48,4 +50,5 @@ for rl in (62, 150):
         st.synchronize()
         ts.append(e0.elapsed_ms(e1))
     ms = min(ts)
-    print(f"query {q.shape[1]} B: {ms:.2f} ms, {cells / ms / 1e6:.1f} G cells/s", flush=True)
+    print(f"band {a.band} query {q.shape[1]} B: {ms:.2f} ms, {cells / ms / 1e6:.1f} G cells/s (full-DP cells)",
+          flush=True)
