@@ -176,8 +176,10 @@ __device__ __forceinline__ void build_lut(const SearchArgs &a, int64_t q, float 
 // set_query for the lean kernel (M = 8, ksub = 256, dsub = 16, 16-B aligned queries): the same
 // per-entry op order as build_lut, with the query sub-vector made wave-uniform (SGPRs) so that only
 // the centroids a lane works on occupy VGPRs. A lane sums 2 H entries of a sub-quantizer at once, their 8 H
-// centroid loads issued together: 16 / H load round trips per LUT. The search takes H = 2 (round 5: C5 search
-// 96.0 -> 95.6 ms, profiles/r05/ab_search_lut_unroll.txt); the builder keeps H = 1 (its 55 VGPRs would double).
+// centroid loads issued together: 16 / H load round trips per LUT. H = 2 measured 96.0 -> 95.6 ms at C5
+// (profiles/r05/ab_search_lut_unroll.txt) but read 13 GB more from HBM per launch (FETCH_SIZE 35.9 -> 48.9 GB,
+// profiles/r05/fetch_lut_halves.txt) and ran no faster under the profiler, so both the search and the builder take
+// H = 1.
 template <int H>
 __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *centroids, float *lut, int lane)
 {
@@ -230,7 +232,7 @@ __device__ __forceinline__ void build_lut_m8_ptr(const float *qv, const float *c
 }
 __device__ __forceinline__ void build_lut_m8(const SearchArgs &a, int64_t q, float *lut, int lane)
 {
-    build_lut_m8_ptr<2>(a.x + q * a.d, a.centroids, lut, lane);
+    build_lut_m8_ptr<1>(a.x + q * a.d, a.centroids, lut, lane);
 }
 
 // greedy_update_nearest on levels max_level .. 1 (HNSW::search, upper levels) [upstream faiss]

@@ -383,6 +383,14 @@ def test_pipeline_cli_c1(tmp_path, c1):
     rc, sc_o, id_o, cnt_o = O.post_process_sw_static(Io, c1["refs"], 150, qbuf, ql, 1, 128, 128)
     assert np.array_equal(np.load(tmp_path / "out" / "sw_scores.npy"), sc_o)
     assert np.array_equal(np.load(tmp_path / "out" / "sw_ids.npy"), id_o)
+    # the opt-in banded SW through the CLI (DRM_SW_BAND, not parity with the reference): the banded oracle's rows
+    r = subprocess.run([os.path.join(ROOT, "bin", "pipeline"), "c1", fq, fna, "128", "128", "5", "out16"],
+                       cwd=tmp_path, env=dict(os.environ, DRM_SW_BAND="16"), capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rc, sc_b, id_b, _ = O.post_process_sw_static(Io, c1["refs"], 150, qbuf, ql, 1, 128, 128, band=16)
+    assert np.array_equal(np.load(tmp_path / "out16" / "sw_scores.npy"), sc_b)
+    assert np.array_equal(np.load(tmp_path / "out16" / "sw_ids.npy"), id_b)
+    assert not np.array_equal(sc_b, sc_o)  # the band is in effect
     r = subprocess.run([os.path.join(ROOT, "bin", "pipeline"), "nope", fq, fna], cwd=tmp_path,
                        capture_output=True, text=True)
     assert r.returncode == 1 and r.stderr.startswith("Error: Config file does not exist")
