@@ -78,7 +78,9 @@ __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_in
 __device__ __forceinline__ int bitlen(uint32_t x) { return 32 - __builtin_clz(x); } // x >= 1
 __device__ __forceinline__ uint32_t dpp_rol1_u32(uint32_t v) // lane i <- lane i+1, lane 63 <- lane 0 (wave_rol:1)
 {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x134, 0xF, 0xF, false);
+    // every lane is written (a rotate), so no "old" value: mov_dpp leaves it undefined, and the v_mov that would
+    // initialise it goes
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint64_t dpp_shr1_u64(uint64_t old, uint64_t v) // lane i <- lane i-1
 {
@@ -319,8 +321,11 @@ struct Heap {
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t mv = ballot(!(val > chv));
         const uint64_t W = pc.path(mv, lm);
-        // per-lane tests: the path is a chain of nodes, so its deepest node is W's highest bit (none: 64)
-        const uint32_t lastW = W ? 63u - (uint32_t)__builtin_clzll(W) : 64u;
+        // per-lane tests: the path is a chain of nodes, so its deepest node is W's highest bit
+        // s_flbit of 0 is -1, so W = 0 gives 63 ^ -1 = -64: no lane and no half, no zero test needed
+        uint32_t fb;
+        asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(W));
+        const uint32_t lastW = fb ^ 63u;
         const bool atlast = (uint32_t)lane == lastW;
         const bool klast = pc.half == lastW;
         // lane (lane >> 1) is on the path and took its L child (lane >> 1 < 32: the low word holds its bit)
@@ -352,7 +357,8 @@ struct Heap {
         // push: h = the chain's ancestors below vnew after the pop: the L halves of lanes 31, 15, 7, 3, 1, 0 (slots 63 ..
         // 1) and lane 63's R (the root, index 7)
         constexpr uint64_t kChainL = (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
-        const uint32_t h = (uint32_t)__builtin_popcountll((ballot(vnew > L) & kChainL) | (ballot(vnew > R) & (1ull << 63)));
+        const uint32_t h = (uint32_t)__builtin_popcount((uint32_t)ballot(vnew > L) & (uint32_t)kChainL) +
+                           (uint32_t)(ballot(vnew > R) >> 63); // 32-bit scalar ops: the chain's L bits are in the low word
         // the chain indices below h take their father's value, index h takes vnew (h = 7: the root)
         const bool sh = pc.cidx < h;
         L = sh ? fl : L;
