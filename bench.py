@@ -18,6 +18,8 @@ Search (`--index`): pq (default), faiss_search(index, emb, k_clusters=K, ef=EF) 
 pipeline's index; flat (C3 only): hnswlib fp32-L2 searchKnn (src/hnswlib_dir/search.cpp:7-52), M=64, EFC=128.
 The timed region excludes inference and file I/O, as the reference's "Search time" window does
 (src/main.cpp:272-285); the encoder, the L2 rerank and the PCIe-inclusive host path are reported beside it.
+`--sw-band W` adds the opt-in banded SW rerank (not parity with the reference) on the same search rows as
+`sw_band_opt_in`; the headline is always the full DP.
 """
 import argparse
 import json

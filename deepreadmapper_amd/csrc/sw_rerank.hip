@@ -767,13 +767,14 @@ __global__ __launch_bounds__(64) void sw_score_band_kernel(RerankArgs a, int rsw
         }
         __syncthreads();
         // the byte profile: copy s, word x holds positions 4x + s .. 4x + s + 3 (query column position - W)
+        const int qn = min(qlen, kBandQMax); // a longer query is refused below; its profile is never read
         for (int it = lane; it < 4 * rsw; it += 64) {
             const int s = it / rsw, x = it - s * rsw;
             uint32_t cq = 0u; // the 4 positions' codes, 0xFF outside the query
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int j = 4 * x + e + s - W;
-                const uint32_t c = (j >= 0 && j < qlen) ? (uint32_t)code_of[qbuf[j]] : 0xFFu;
+                const uint32_t c = (j >= 0 && j < qn) ? (uint32_t)code_of[qbuf[j]] : 0xFFu;
                 cq |= c << (8 * e);
             }
 #pragma unroll
