@@ -50,6 +50,19 @@ __device__ __forceinline__ uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32
 __device__ __forceinline__ uint32_t lo32(uint64_t v) { return (uint32_t)v; }
 __device__ __forceinline__ int32_t unpack_id(uint64_t v) { return (int32_t)(lo32(v) ^ 0x80000000u); }
 __device__ __forceinline__ int32_t readlane32(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// llvm.amdgcn.writelane (this clang has no builtin for it): old with lane `lane` (wave-uniform, mod 64) replaced by
+// the wave-uniform val -- one v_writelane_b32, no compare and no copy of val into a VGPR
+extern "C" __device__ int drm_llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ int32_t writelane32(int32_t v, int32_t s, uint32_t l)
+{
+    return drm_llvm_writelane(s, (int)(l & 63u), v);
+}
+__device__ __forceinline__ uint64_t writelane64(uint64_t v, uint64_t s, uint32_t l)
+{
+    const uint32_t h = (uint32_t)drm_llvm_writelane((int)(s >> 32), (int)(l & 63u), (int)(v >> 32));
+    const uint32_t o = (uint32_t)drm_llvm_writelane((int)(uint32_t)s, (int)(l & 63u), (int)(uint32_t)v);
+    return ((uint64_t)h << 32) | o;
+}
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 {
     const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hi32(v), l);
@@ -326,24 +339,27 @@ struct Heap {
         uint32_t fb;
         asm("s_flbit_i32_b64 %0, %1" : "=s"(fb) : "s"(W));
         const uint32_t lastW = fb ^ 63u;
-        const bool atlast = (uint32_t)lane == lastW;
-        const bool klast = pc.half == lastW;
         // lane (lane >> 1) is on the path and took its L child (lane >> 1 < 32: the low word holds its bit)
-        const bool moved = ((uint32_t)(W & lm) >> pc.half) & 1u;
-        // lane 0: the root after the pop -- node 0's chosen child if node 0 is on the path (lane 0's own bit of W),
-        // else slot 127's value
-        const bool onw = in_mask(W);
-        const uint64_t rootpp = onw ? chv : val;
-        const int32_t rootppI = onw ? chI : valI;
-        // the chain's fathers after the pop, from the pre-pop registers; lane 0's father is the root
+        const uint32_t wlm = (uint32_t)(W & lm);
+        const bool moved = (wlm >> pc.half) & 1u;
+        // the single-lane writes of slot 127's value (val) are v_writelanes of the scalar, not a compare and a select
+        // of a VGPR copy. Lane 0: the root after the pop -- node 0's chosen child if node 0 is on the path, else val
+        // (only lane 0 is read: with node 0 on the path val goes to lane 1)
+        const uint64_t rootpp = writelane64(chv, val, (uint32_t)W & 1u);
+        const int32_t rootppI = writelane32(chI, valI, (uint32_t)W & 1u);
+        // the chain's fathers after the pop, from the pre-pop registers (read on the chain lanes 0, 1, 3, 7, 15, 31,
+        // 63 only): the moved child, or L before the pop; chain lane 2 lastW + 1 takes val when the path's end took
+        // its L child (else the write goes to lane 2, off the chain); lane 0's father is the root
+        const uint32_t kl = (lastW < 32u && ((wlm >> (lastW & 31u)) & 1u)) ? 2u * lastW + 1u : 2u;
+        uint64_t fl = writelane64(moved ? chv : fpre, val, kl);
+        int32_t flI = writelane32(moved ? chI : fpreI, valI, kl);
         const bool s1 = in_mask(1ull);
-        uint64_t fl = moved ? (klast ? val : chv) : fpre;
-        int32_t flI = moved ? (klast ? valI : chI) : fpreI;
         fl = s1 ? rootpp : fl;
         flI = s1 ? rootppI : flI;
-        // pop writes: the path nodes' chosen child slots, and the root
-        const uint64_t up = atlast ? val : up0;
-        const int32_t upI = atlast ? valI : up0I;
+        // pop writes: the path nodes' chosen child slots (the path's end takes val; with no path the write to lane
+        // 0 is never read), and the root
+        const uint64_t up = writelane64(up0, val, lastW);
+        const int32_t upI = writelane32(up0I, valI, lastW);
         const bool wl = in_mask(W & lm), wr = in_mask(W & ~lm);
         L = wl ? up : L;
         IL = wl ? upI : IL;
@@ -359,16 +375,17 @@ struct Heap {
         constexpr uint64_t kChainL = (1ull << 31) | (1ull << 15) | (1ull << 7) | (1ull << 3) | (1ull << 1) | 1ull;
         const uint32_t h = (uint32_t)__builtin_popcount((uint32_t)ballot(vnew > L) & (uint32_t)kChainL) +
                            (uint32_t)(ballot(vnew > R) >> 63); // 32-bit scalar ops: the chain's L bits are in the low word
-        // the chain indices below h take their father's value, index h takes vnew (h = 7: the root)
+        // index h takes vnew: chain lane (64 >> h) - 1's L (h = 7 writes lane 63's L, which the next select restores),
+        // or lane 63's R (the root) when h = 7; the chain indices below h take their father's value
+        L = writelane64(L, vnew, (64u >> h) - 1u);
+        IL = writelane32(IL, vnewI, (64u >> h) - 1u);
         const bool sh = pc.cidx < h;
         L = sh ? fl : L;
         IL = sh ? flI : IL;
-        const bool xs = pc.cidx == h;
-        L = xs ? vnew : L;
-        IL = xs ? vnewI : IL;
-        const bool xr = s63 && h == 7u;
-        R = xr ? vnew : R;
-        IR = xr ? vnewI : IR;
+        if (h == 7u) {
+            R = writelane64(R, vnew, 63u);
+            IR = writelane32(IR, vnewI, 63u);
+        }
     }
 
     // faiss heap_push(k, val) while the ef = 128 heap fills (2 <= k <= 128): val enters slot k - 1 and sifts up its
