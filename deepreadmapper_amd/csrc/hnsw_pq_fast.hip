@@ -350,7 +350,9 @@ struct Heap {
         // the chain's fathers after the pop, from the pre-pop registers (read on the chain lanes 0, 1, 3, 7, 15, 31,
         // 63 only): the moved child, or L before the pop; chain lane 2 lastW + 1 takes val when the path's end took
         // its L child (else the write goes to lane 2, off the chain); lane 0's father is the root
-        const uint32_t kl = (lastW < 32u && ((wlm >> (lastW & 31u)) & 1u)) ? 2u * lastW + 1u : 2u;
+        // (one 64-bit bit test: the low word of W & lm, zero-extended, so a path end at lane >= 32 -- or no path --
+        // tests a zero bit)
+        const uint32_t kl = (((uint64_t)wlm >> (lastW & 63u)) & 1u) ? 2u * lastW + 1u : 2u;
         uint64_t fl = writelane64(moved ? chv : fpre, val, kl);
         int32_t flI = writelane32(moved ? chI : fpreI, valI, kl);
         const bool s1 = in_mask(1ull);
