@@ -389,16 +389,28 @@ def gather_results(D, dev, n_total, bufs):
     ndev = device_count()
     if D.world > ndev:  # RCCL needs one GPU per rank (drm_comm_init: DRM_ERR_UNSUPPORTED)
         return {"skipped": f"{D.world} ranks share {ndev} device(s): the RCCL gather needs one GPU per rank"}
-    try:
-        from deepreadmapper_amd.device import DeviceBuffer, synchronize
-        from deepreadmapper_amd.executor import Comm
-        if D.comm is None:
+    # the unique-id broadcast and the checksum exchange are collectives on the gloo control plane: every rank reaches
+    # them whatever happened to its own gather (an error is carried in the exchange), so a failing rank cannot leave
+    # the others waiting in a collective it never enters
+    from deepreadmapper_amd.device import DeviceBuffer, synchronize
+    from deepreadmapper_amd.executor import Comm
+    obj = [None]
+    if D.comm is None:
+        try:
             obj = [Comm.unique_id() if D.rank == 0 else None]
-            D.dist.broadcast_object_list(obj, src=0)
+        except Exception as e:  # noqa: BLE001
+            obj = [None]
+            log(f"[bench] rank 0: RCCL unique id failed: {e}")
+        D.dist.broadcast_object_list(obj, src=0)
+    out, full, local = {}, {}, None
+    try:
+        if D.comm is None:
+            if obj[0] is None:
+                raise RuntimeError("no RCCL unique id from rank 0")
             D.comm = Comm(obj[0], D.world, D.rank, dev)
         synchronize()
         t0 = time.perf_counter()
-        full, nbytes = {}, 0
+        nbytes = 0
         for name, b in bufs:
             row = b.nbytes // b.shape[0]
             recv = DeviceBuffer((n_total,) + tuple(b.shape[1:]), b.dtype) if D.rank == 0 else None
@@ -409,13 +421,16 @@ def gather_results(D, dev, n_total, bufs):
         ms = (time.perf_counter() - t0) * 1e3
         out = {"backend": "RCCL (drm_comm_gather_rows, C++)", "ms": round(ms, 3), "bytes_per_rank": int(nbytes)}
         local = {name: b.checksum() for name, b in bufs}
-        match = shard_checksums(D, n_total, local, lambda lo, hi: {k: v.checksum(lo, hi) for k, v in full.items()})
-        if D.rank == 0:
-            out["shards_match"] = match
-            out["rows"] = int(n_total)
-        return out
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-        return {"error": f"{type(e).__name__}: {e}"}
+        out = {"error": f"{type(e).__name__}: {e}"}
+        local = None
+    ok0 = "error" not in out
+    match = shard_checksums(D, n_total, local, (lambda lo, hi: {k: v.checksum(lo, hi) for k, v in full.items()})
+                            if ok0 else (lambda lo, hi: None))
+    if D.rank == 0 and ok0:
+        out["shards_match"] = match
+        out["rows"] = int(n_total)
+    return out
 
 
 def shard_checksums(D, n_total, local_sums, slice_sums):
@@ -427,7 +442,8 @@ def shard_checksums(D, n_total, local_sums, slice_sums):
     D.dist.all_gather_object(sums, local_sums)
     if D.rank != 0:
         return None
-    return [slice_sums(*shard_range(n_total, r, D.world)) == sums[r] for r in range(D.world)]
+    # a rank whose gather failed sends None: its shard does not match
+    return [sums[r] is not None and slice_sums(*shard_range(n_total, r, D.world)) == sums[r] for r in range(D.world)]
 
 
 def gather_verdict(D, gather):
