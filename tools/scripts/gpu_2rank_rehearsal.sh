@@ -5,5 +5,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 1100 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29521 \
-  bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-host-path --no-encoder --no-l2 > gpurun_out/bench_2rank_r04.json 2> gpurun_out/bench_2rank_r04.err || { echo FAILED; tail -30 gpurun_out/bench_2rank_r04.err; exit 1; }
-cat gpurun_out/bench_2rank_r04.json
+  bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-host-path --no-encoder --no-l2 > gpurun_out/bench_2rank_${TAG:-r05}.json 2> gpurun_out/bench_2rank_${TAG:-r05}.err || { echo FAILED; tail -30 gpurun_out/bench_2rank_${TAG:-r05}.err; exit 1; }
+cat gpurun_out/bench_2rank_${TAG:-r05}.json
