@@ -770,7 +770,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             uint32_t d0 = ufirst(dhint);
             uint64_t eqm = ballot(pk == d0);
             const uint64_t ltm = ballot(pk < d0);
-            if (ltm != 0ull || eqm == 0ull) {
+            // one scalar test: a slot under the hint, or none at it (the compiler's own form of the two tests takes
+            // seven scalar instructions)
+            uint64_t bad;
+            asm("s_cmp_eq_u64 %1, 0\n\ts_cselect_b64 %0, 1, 0\n\ts_or_b64 %0, %0, %2" : "=&s"(bad) : "s"(eqm), "s"(ltm) : "scc");
+            if (bad != 0ull) {
                 d0 = wave_min_u32(pk);
                 eqm = ballot(pk == d0);
             }
@@ -883,7 +887,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             // below the root was seen iff it is in the heap (popped or not): a seen link either entered the heap
             // and is still there, or was rejected / evicted at a root that is now at or below its distance.
             uint64_t rem = actm;
-            if (kc < ef) { // the heap fills: every link not in it is pushed
+            if (__builtin_expect(kc < ef, 0)) { // the heap fills: every link not in it is pushed
                 while (rem) {
                     const int l = __builtin_ctzll(rem);
                     asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
