@@ -33,7 +33,7 @@ $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 # 1-2 % slower under it, so only this file (profiles/r04/ab_search_sched_strategy.txt); loops aligned to 16 bytes:
 # 103.7 -> 103.5 ms (64: 103.9, profiles/r04/ab_search_loop_align.txt)
 $(BUILD)/hnsw_pq_fast.o: $(SRC)/hnsw_pq_fast.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=max-ilp -falign-loops=16 -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -falign-loops=16 -c $< -o $@
 
 $(BUILD)/capi.o: $(SRC)/capi.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
