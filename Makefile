@@ -29,11 +29,16 @@ $(BUILD):
 $(BUILD)/%.o: $(SRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# the search kernel under the max-ILP machine scheduler: 104.3 -> 103.7 ms at C5, ids identical; the SW rerank is
-# 1-2 % slower under it, so only this file (profiles/r04/ab_search_sched_strategy.txt); loops aligned to 16 bytes:
-# 103.7 -> 103.5 ms (64: 103.9, profiles/r04/ab_search_loop_align.txt)
+# the search kernel: loops aligned to 16 bytes (103.7 -> 103.5 ms at C5, profiles/r04/ab_search_loop_align.txt);
+# the default machine scheduler (max-ILP, kept in round 4, is 0.8 % slower with the round-5 code,
+# profiles/r05/ab_search_sched_strategy_r05*.txt)
 $(BUILD)/hnsw_pq_fast.o: $(SRC)/hnsw_pq_fast.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -falign-loops=16 -c $< -o $@
+
+# the SW rerank under the iterative-ILP machine scheduler: 28.1 -> 27.6 ms on the 152-column probe, equal at 64
+# (profiles/r05/ab_sw_sched_strategy.txt)
+$(BUILD)/sw_rerank.o: $(SRC)/sw_rerank.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=iterative-ilp -c $< -o $@
 
 $(BUILD)/capi.o: $(SRC)/capi.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
