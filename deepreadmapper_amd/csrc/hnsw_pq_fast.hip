@@ -678,13 +678,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
         Heap hp;
         hp.L = kUnused;
         hp.R = lane == 63 ? pack(dn, nearest) : kUnused;
-        hp.IL = -1;
-        hp.IR = lane == 63 ? nearest : -1;
+        // node ids are held tagged (id ^ 2^31, the low word of their key): the pushed key's low word is the id as read,
+        // no scalar XOR per push; an empty slot holds the tag of -1
+        hp.IL = (int32_t)0x7FFFFFFF;
+        hp.IR = lane == 63 ? (int32_t)((uint32_t)nearest ^ 0x80000000u) : (int32_t)0x7FFFFFFF;
         int kc = 1;
         // the root's key (high word) and node id, current whenever the heap is full (kc == ef): the fill does not track
         // them, they are read from lane 63's R once the heap is full, and after every full-heap replace
         uint32_t rootHi = dn;
-        int32_t rootI = nearest;
+        int32_t rootI = (int32_t)((uint32_t)nearest ^ 0x80000000u); // tagged
         // result set: the log (LOGRES) or a sorted register set of k <= 64 entries
         int logn = 0;
         uint64_t rv = ~0ull; // !LOGRES: lane j < k holds the j-th smallest (key, id) so far
@@ -823,6 +825,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 praw = load_link_raw(a.rows + (size_t)v0 * (size_t)a.row_words, lane, deg0);
             const int32_t v1 = lane < deg0 ? (int32_t)praw.x : -1;
             const uint2 c8 = make_uint2(praw.y, praw.z); // past deg0: link 0's code (the LUT reads stay in the LUT)
+            const int32_t v1x = (int32_t)((uint32_t)v1 ^ 0x80000000u); // the links' ids tagged, as the heap holds them
             const uint64_t negm = ballot(v1 < 0);
             const int jmax = negm ? __builtin_ctzll(negm) : 64; // lanes past deg0 hold -1
             const uint64_t actm = negm ? (negm & (0ull - negm)) - 1ull : ~0ull;
@@ -892,12 +895,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                     const int l = __builtin_ctzll(rem);
                     asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
                     const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
-                    const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                    const int32_t idl = __builtin_amdgcn_readlane(v1x, l); // tagged
                     if (STAMPS)
                         st_acc[4] += 1u; // links tested against the heap's ids
                     if (hp.holds(idl))
                         continue;
-                    const uint64_t val = pack(key, idl);
+                    const uint64_t val = ((uint64_t)key << 32) | (uint32_t)idl;
                     DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, 0u, (uint32_t)sn);
                     if (!LOGRES && key < thr)
                         add_result(val);
@@ -918,12 +921,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 const int l = __builtin_ctzll(rem);
                 asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(l)); // rem &= rem - 1, one scalar op
                 const uint32_t key = (uint32_t)__builtin_amdgcn_readlane((int)dall, l);
-                const int32_t idl = __builtin_amdgcn_readlane(v1, l);
+                const int32_t idl = __builtin_amdgcn_readlane(v1x, l); // tagged
                 if (STAMPS)
                     st_acc[4] += 1u;
                 if (hp.holds(idl))
                     continue;
-                const uint64_t val = pack(key, idl);
+                const uint64_t val = ((uint64_t)key << 32) | (uint32_t)idl;
                 DRM_DBG(4u, q, nstep, (uint32_t)idl, key, (uint32_t)kc, 0u, (uint32_t)sn);
                 if (!LOGRES && key < thr)
                     add_result(val);
@@ -948,7 +951,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                         log_flush();
                     const bool at = lane == sn; // lane sn takes the entry (one compare, two selects)
                     sbh = at ? evk : sbh;
-                    sbl = at ? (uint32_t)evi ^ 0x80000000u : sbl;
+                    sbl = at ? (uint32_t)evi : sbl; // already tagged
                     ++sn;
                 }
             }
@@ -968,14 +971,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             if (logn + kc > a.log_cap)
                 log_compact();
             {
-                const bool hl = hp.IL >= 0, hr = hp.IR >= 0;
+                const bool hl = hp.IL != (int32_t)0x7FFFFFFF, hr = hp.IR != (int32_t)0x7FFFFFFF; // filled slots
                 const uint64_t mL = ballot(hl), mR = ballot(hr), below = lanes_below(lane);
                 if (hl)
-                    __hip_atomic_store(lg + logn + __builtin_popcountll(mL & below), pack(hi32(hp.L), hp.IL),
+                    __hip_atomic_store(lg + logn + __builtin_popcountll(mL & below), ((uint64_t)hi32(hp.L) << 32) | (uint32_t)hp.IL,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (hr)
                     __hip_atomic_store(lg + logn + __builtin_popcountll(mL) + __builtin_popcountll(mR & below),
-                                       pack(hi32(hp.R), hp.IR), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                       ((uint64_t)hi32(hp.R) << 32) | (uint32_t)hp.IR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef DRM_PQ_DEBUG
                 if (__builtin_popcountll(mL) + __builtin_popcountll(mR) != kc && lane == 0)
                     printf("[pq dbg] q %d: %d heap slots hold an id, %d filled\n", q,
