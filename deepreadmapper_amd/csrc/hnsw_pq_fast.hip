@@ -133,9 +133,11 @@ __device__ __forceinline__ uint32_t adc8(const float *lut, uint2 c)
     lv[6] = *reinterpret_cast<const float *>(b + bx4<2>(c.y) + 6144);
     lv[7] = *reinterpret_cast<const float *>(b + bx4<3>(c.y) + 7168);
     __builtin_amdgcn_sched_barrier(0);
-    float r = 0.0f;
+    // faiss sums from +0.0; +0.0 + x == x for every LUT entry (a sum of squares from +0.0: never -0.0), so the sum
+    // starts at the first entry (one add fewer, the same bits)
+    float r = lv[0];
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+    for (int m = 1; m < 8; ++m)
         r = __fadd_rn(r, lv[m]);
     // ord32 of a sum of non-negative LUT entries (squared sub-distances, summed from +0.0): the sign bit is clear,
     // so ord32(r) is r's bit pattern with the sign bit set -- one op instead of ord32's select
@@ -470,7 +472,7 @@ __device__ __forceinline__ void greedy_upper_inl(const SearchArgs &a, const floa
                                                  uint32_t &dn_out, int &ndis_out, int &nhops_out)
 {
     int32_t nearest = a.entry_point;
-    uint32_t dn = ufirst(ord32(pq_distance_code<true>(a, lut, nearest, load_code8<true>(a, nearest))));
+    uint32_t dn = ufirst(ord32_nonneg(pq_distance_code<true>(a, lut, nearest, load_code8<true>(a, nearest))));
     int ndis = 0, nhops = 0;
     for (int level = a.max_level; level >= 1; --level) {
         const int cnt = a.cum[level + 1] - a.cum[level];
@@ -487,7 +489,7 @@ __device__ __forceinline__ void greedy_upper_inl(const SearchArgs &a, const floa
             const int nvalid = neg ? (__ffsll((unsigned long long)neg) - 1) : cnt;
             uint32_t dk = 0xFFFFFFFFu;
             if (lane < nvalid)
-                dk = ord32(pq_distance_code<true>(a, lut, v, c8));
+                dk = ord32_nonneg(pq_distance_code<true>(a, lut, v, c8));
             ndis += nvalid;
             nhops += 1;
             // sequential `if (dis < d_nearest)` in link order == the first lane holding the minimum: a DPP min over the

@@ -23,6 +23,8 @@ __device__ __forceinline__ uint32_t ord32(float f)
     uint32_t u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+// ord32 of a value known to have its sign bit clear (a PQ-ADC distance: a sum of non-negative LUT entries from +0.0)
+__device__ __forceinline__ uint32_t ord32_nonneg(float f) { return __float_as_uint(f) | 0x80000000u; }
 __device__ __forceinline__ float unord32(uint32_t o)
 {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
@@ -83,8 +85,10 @@ __device__ __forceinline__ float pq_distance_code(const SearchArgs &a, const flo
 {
     float r = 0.0f;
     if (FAST8) { // M == 8, nbits == 8: the 8-byte code is already in c8
+        // +0.0 + x == x for a LUT entry (never -0.0): the sum starts at the first entry, the same bits
+        r = lut[c8.x & 255u];
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+        for (int m = 1; m < 4; ++m)
             r = __fadd_rn(r, lut[m * 256 + ((c8.x >> (8 * m)) & 255u)]);
 #pragma unroll
         for (int m = 0; m < 4; ++m)
