@@ -376,6 +376,64 @@ def host_path(ix, table, q_emb, queries, K, EF, flat):
             "note": "drm_search_rerank, pinned host in/out, one rank, PCIe-inclusive (not the metric)"}
 
 
+def comm_unique_id(D):
+    """Rank 0's RCCL unique id, broadcast over the gloo control plane (None if it failed, or if rank 0's
+    communicator exists already). Collective, whatever state a rank is in: every rank calls it at the same point."""
+    from deepreadmapper_amd.executor import Comm
+    obj = [None]
+    if D.rank == 0 and D.comm is None:
+        try:
+            obj = [Comm.unique_id()]
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] rank 0: RCCL unique id failed: {e}")
+    D.dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def ensure_comm(D, dev, uid):
+    """The job's RCCL communicator (drm_comm), created once from comm_unique_id's id."""
+    if D.comm is None:
+        from deepreadmapper_amd.executor import Comm
+        if uid is None:
+            raise RuntimeError("no RCCL unique id from rank 0")
+        D.comm = Comm(uid, D.world, D.rank, dev)
+    return D.comm
+
+
+def load_index(args, D, path, dev):
+    """The C5/C3 index replica of this rank. N > 1 with one GPU per rank (args.index_bcast, the default): rank 0
+    parses the IHNp file and drm_index_broadcast replicates it over RCCL, each receiver
+    checking the root's buffer checksums; otherwise, or if the broadcast failed on any rank (the ranks agree on that
+    over gloo), every rank loads the file itself. Returns (index, {how the replica was made})."""
+    from deepreadmapper_amd.device import device_count
+    from deepreadmapper_amd.search import HnswPqIndex
+    t0 = time.time()
+    if D.world == 1 or not args.index_bcast or D.world > device_count():
+        why = "one rank" if D.world == 1 else ("--no-index-bcast" if not args.index_bcast else
+                                                 "ranks share a device (RCCL needs one GPU per rank)")
+        ix = HnswPqIndex(path, dev)
+        return ix, {"mode": "file per rank", "why": why, "s": round(time.time() - t0, 2)}
+    uid = comm_unique_id(D)
+    ix, err = None, None
+    try:
+        comm = ensure_comm(D, dev, uid)
+        root_ix = HnswPqIndex(path, dev) if D.rank == 0 else None
+        t_load = time.time() - t0
+        t1 = time.time()
+        ix = HnswPqIndex.broadcast(comm, root_ix, root=0)
+        t_bcast = time.time() - t1
+    except Exception as e:  # noqa: BLE001 -- every rank then falls back together
+        err = f"{type(e).__name__}: {e}"
+        log(f"[bench] rank {D.rank}: index broadcast failed: {err}")
+    if D.allreduce(1.0 if err else 0.0, "SUM") > 0:
+        if ix is not None:
+            ix.free()
+        ix = HnswPqIndex(path, dev)
+        return ix, {"mode": "file per rank", "why": "broadcast failed", "error": err, "s": round(time.time() - t0, 2)}
+    return ix, {"mode": "rccl broadcast (drm_index_broadcast)", "root_load_s": round(t_load, 2),
+                "broadcast_s": round(t_bcast, 2), "device_bytes": int(ix.info.device_bytes)}
+
+
 def gather_results(D, dev, n_total, bufs):
     """End-of-run exchange: every rank's device-resident result rows are gathered to
     rank 0 over RCCL by the library's own C++ path (drm_comm_gather_rows: grouped ncclSend/ncclRecv over
@@ -393,21 +451,10 @@ def gather_results(D, dev, n_total, bufs):
     # them whatever happened to its own gather (an error is carried in the exchange), so a failing rank cannot leave
     # the others waiting in a collective it never enters
     from deepreadmapper_amd.device import DeviceBuffer, synchronize
-    from deepreadmapper_amd.executor import Comm
-    obj = [None]
-    if D.comm is None:
-        try:
-            obj = [Comm.unique_id() if D.rank == 0 else None]
-        except Exception as e:  # noqa: BLE001
-            obj = [None]
-            log(f"[bench] rank 0: RCCL unique id failed: {e}")
-        D.dist.broadcast_object_list(obj, src=0)
+    uid = comm_unique_id(D)
     out, full, local = {}, {}, None
     try:
-        if D.comm is None:
-            if obj[0] is None:
-                raise RuntimeError("no RCCL unique id from rank 0")
-            D.comm = Comm(obj[0], D.world, D.rank, dev)
+        ensure_comm(D, dev, uid)
         synchronize()
         t0 = time.perf_counter()
         nbytes = 0
@@ -615,6 +662,9 @@ def main():
     ap.add_argument("--index", choices=["pq", "flat"], default="pq",
                     help="pq (default): faiss IndexHNSWPQ, the live pipeline's index (src/main.cpp:236-237); flat: "
                          "hnswlib fp32-L2 index (M=64, EFC=128, the reference's hnswlib defaults) over the C3 windows")
+    ap.add_argument("--index-bcast", action=argparse.BooleanOptionalAction, default=True,
+                    help="N > 1 (one GPU per rank): rank 0 loads the index file and drm_index_broadcast replicates it "
+                         "over RCCL (default); --no-index-bcast: every rank parses the file itself")
     ap.add_argument("--sw-band", type=int, default=0, choices=[0, 8, 16, 32],
                     help="also time the opt-in banded SW rerank (drm_refs_set_sw_band, NOT parity with the reference) on "
                          "the same search rows, reported beside the headline as `sw_band_opt_in`; 0 = skip")
@@ -664,11 +714,12 @@ def main():
             log(f"[bench] hnswlib fp32 index built in {time.time() - t0:.1f}s")
         D.barrier()
         ix = HnswFlatIndex(fpath, dev)
+        replication = {"mode": "file per rank", "why": "hnswlib index"}
         d_L = DeviceBuffer((Q, K), np.uint64)
     else:
         t0 = time.time()
-        ix = HnswPqIndex(wl["index_path"], dev)
-        log(f"[bench] index loaded in {time.time() - t0:.1f}s")
+        ix, replication = load_index(args, D, wl["index_path"], dev)
+        log(f"[bench] index replica ready in {time.time() - t0:.1f}s: {replication}")
     t0 = time.time()
     table = WindowTable(refs, dev)
     log(f"[bench] window table ({len(refs)} x {refs.shape[1]} B) uploaded in {time.time() - t0:.1f}s")
@@ -864,6 +915,7 @@ def main():
                                           "source": "profiles/r04/valu_rate_mix.txt (the DP's instruction mix alone, "
                                                     "all operands in registers; the kernel holds 2 waves per SIMD)"}},
             "cpu_baseline": cpu,
+            "index_replication": replication,
             "gather": gather,
             "gather_ok": gather_ok,
             "host_path": host,

@@ -78,7 +78,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__global__ __launch_bounds__(256) void checksum_kernel(const uint8_t *p, int64_t nbytes, unsigned long long *out)
+// one partial sum per wave, stored (no atomics, no zero-fill to order before them); the host adds the partials
+__global__ __launch_bounds__(256) void checksum_kernel(const uint8_t *p, int64_t nbytes, unsigned long long *partial)
 {
     const int64_t nw = (nbytes + 7) >> 3;
     uint64_t acc = 0;
@@ -96,7 +97,28 @@ __global__ __launch_bounds__(256) void checksum_kernel(const uint8_t *p, int64_t
     for (int o = 32; o > 0; o >>= 1)
         acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0)
-        atomicAdd(out, (unsigned long long)acc);
+        partial[blockIdx.x * 4 + (threadIdx.x >> 6)] = (unsigned long long)acc;
+}
+
+// drm_device_checksum's sum, on `s`; returns once it is known. Plain synchronous allocation and copies: the
+// stream-ordered pool form (hipMallocAsync + hipMemsetAsync + atomics + an async copy into pageable memory) returned
+// stale sums on the box after unrelated allocations (drm_index_broadcast)
+uint64_t device_checksum(const void *d_ptr, int64_t nbytes, hipStream_t s)
+{
+    const int64_t nw = (nbytes + 7) >> 3;
+    if (nw == 0)
+        return 0;
+    const int64_t blocks = std::min<int64_t>((nw + 255) / 256, 4096);
+    DevBuf<unsigned long long> partial((size_t)blocks * 4);
+    hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint8_t *)d_ptr, nbytes, partial.p);
+    DRM_HIP_CHECK(hipGetLastError());
+    DRM_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h((size_t)blocks * 4);
+    partial.download(h.data());
+    uint64_t sum = 0;
+    for (unsigned long long v : h)
+        sum += (uint64_t)v;
+    return sum;
 }
 
 template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
@@ -108,6 +130,40 @@ template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
         DRM_HIP_CHECK(hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
     bytes += (int64_t)nb;
     return p;
+}
+
+// tuning knobs read when an index is loaded or received: kernel choice, occupancy, diagnostics, the
+// safety bounds (tests lower them)
+void apply_load_env(drm::DeviceIndex &d)
+{
+    if (const char *e = std::getenv("DRM_SEARCH_HOP_BOUND"))
+        d.hop_bound = std::max<int64_t>(0, std::atoll(e));
+    if (const char *e = std::getenv("DRM_WAVE_ITEM_BOUND"))
+        d.item_bound = std::max<int64_t>(0, std::atoll(e));
+    if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
+        d.waves_per_cu = std::max(1, std::atoi(e));
+    d.waves_per_cu_load = d.waves_per_cu;
+    if (const char *e = std::getenv("DRM_SEARCH_EXACT_STATS"))
+        d.exact_stats = std::atoi(e) ? 1 : 0;
+    if (const char *e = std::getenv("DRM_SEARCH_LOG_CAP"))
+        d.log_cap_req = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("DRM_SEARCH_FAST"))
+        d.use_fast = std::atoi(e) ? 1 : 0;
+    if (const char *e = std::getenv("DRM_SEARCH_INLINE"))
+        d.use_inline = std::atoi(e) ? 1 : 0;
+    if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
+        d.force_lds_kernel = std::atoi(e) ? 1 : 0;
+    if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
+        if (std::atoi(e)) {
+            DRM_HIP_CHECK(hipMalloc(&d.stamps, 12 * sizeof(uint64_t)));
+            DRM_HIP_CHECK(hipMemset(d.stamps, 0, 12 * sizeof(uint64_t)));
+        }
+    if (const char *e = std::getenv("DRM_SEARCH_TRACE"))
+        if (std::atoi(e)) { // host memory the device writes through: readable while a kernel runs (or hangs)
+            DRM_HIP_CHECK(hipHostMalloc((void **)&d.trace, sizeof(uint32_t) * drm::kTraceWords,
+                                        hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset(d.trace, 0, sizeof(uint32_t) * drm::kTraceWords);
+        }
 }
 
 void free_index(drm::DeviceIndex &d)
@@ -174,21 +230,7 @@ int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *
     return guarded([&] {
         if (!out || nbytes < 0 || (nbytes > 0 && (!d_ptr || ((uintptr_t)d_ptr & 7u) != 0u)))
             throw Error(DRM_ERR_ARG, "drm_device_checksum: needs an 8-byte aligned device pointer and an output");
-        hipStream_t s = (hipStream_t)stream;
-        unsigned long long *d_out = nullptr;
-        DRM_HIP_CHECK(hipMallocAsync((void **)&d_out, sizeof(*d_out), s));
-        DRM_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(*d_out), s));
-        const int64_t nw = (nbytes + 7) >> 3;
-        if (nw > 0) {
-            const int64_t blocks = std::min<int64_t>((nw + 255) / 256, 4096);
-            hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint8_t *)d_ptr, nbytes, d_out);
-            DRM_HIP_CHECK(hipGetLastError());
-        }
-        unsigned long long h = 0;
-        DRM_HIP_CHECK(hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, s));
-        DRM_HIP_CHECK(hipFreeAsync(d_out, s));
-        DRM_HIP_CHECK(hipStreamSynchronize(s));
-        *out = (uint64_t)h;
+        *out = device_checksum(d_ptr, nbytes, (hipStream_t)stream);
     });
 }
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes)
@@ -311,35 +353,7 @@ int drm_index_load(const char *path, int device, drm_index **out)
             }
         }
         d.upper_len = (int64_t)upper.size();
-        // tuning knobs: kernel choice, occupancy, diagnostics; the safety bounds (tests lower them)
-        if (const char *e = std::getenv("DRM_SEARCH_HOP_BOUND"))
-            d.hop_bound = std::max<int64_t>(0, std::atoll(e));
-        if (const char *e = std::getenv("DRM_WAVE_ITEM_BOUND"))
-            d.item_bound = std::max<int64_t>(0, std::atoll(e));
-        if (const char *e = std::getenv("DRM_SEARCH_WAVES_PER_CU"))
-            d.waves_per_cu = std::max(1, std::atoi(e));
-        d.waves_per_cu_load = d.waves_per_cu;
-        if (const char *e = std::getenv("DRM_SEARCH_EXACT_STATS"))
-            d.exact_stats = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_LOG_CAP"))
-            d.log_cap_req = std::max(1, std::atoi(e));
-        if (const char *e = std::getenv("DRM_SEARCH_FAST"))
-            d.use_fast = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_INLINE"))
-            d.use_inline = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_LDS_KERNEL"))
-            d.force_lds_kernel = std::atoi(e) ? 1 : 0;
-        if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
-            if (std::atoi(e)) {
-                DRM_HIP_CHECK(hipMalloc(&d.stamps, 12 * sizeof(uint64_t)));
-                DRM_HIP_CHECK(hipMemset(d.stamps, 0, 12 * sizeof(uint64_t)));
-            }
-        if (const char *e = std::getenv("DRM_SEARCH_TRACE"))
-            if (std::atoi(e)) { // host memory the device writes through: readable while a kernel runs (or hangs)
-                DRM_HIP_CHECK(hipHostMalloc((void **)&d.trace, sizeof(uint32_t) * drm::kTraceWords,
-                                            hipHostMallocMapped | hipHostMallocCoherent));
-                std::memset(d.trace, 0, sizeof(uint32_t) * drm::kTraceWords);
-            }
+        apply_load_env(d);
         try {
             d.centroids = upload_vec(h.centroids, d.device_bytes);
             d.codes = upload_vec(h.codes, d.device_bytes);
@@ -363,6 +377,203 @@ int drm_index_load(const char *path, int device, drm_index **out)
         d.meta.pq_nbits = h.pq_nbits;
         d.meta.cum_nneighbor_per_level = h.cum_nneighbor_per_level;
         *out = ix.release();
+    });
+}
+
+} // extern "C"
+
+// drm_index_broadcast: the wire header the root sends first -- every scalar a DeviceIndex and its kept metadata hold,
+// the byte size of each buffer that follows, and the root's checksum of each (receivers verify what arrived)
+namespace {
+constexpr uint64_t kBcastMagic = 0x3143425849524444ull; // "DDRIXBC1"
+constexpr int kBcastBufs = 5;                          // centroids, codes, nbr0, upper_off, upper_nbr
+struct IndexWire {
+    uint64_t magic;
+    int32_t d, pq_M, pq_nbits, dsub, ksub, code_size, deg0, n_levels, max_level, entry_point, has_dup_links;
+    int32_t cum[drm::kMaxLevels + 1];
+    int64_t ntotal, upper_len;
+    int32_t hdr_d, hdr_metric_type;
+    int64_t hdr_ntotal;
+    float hdr_metric_arg;
+    int32_t hdr_is_trained, efConstruction, efSearch;
+    uint64_t meta_pq_M, meta_pq_nbits;
+    uint64_t bytes[kBcastBufs], sums[kBcastBufs];
+};
+
+// the byte size upload_vec gives each buffer (at least one element)
+void index_buffer_sizes(const drm::DeviceIndex &d, uint64_t *bytes)
+{
+    bytes[0] = sizeof(float) * (uint64_t)std::max<int64_t>((int64_t)d.pq_M * d.ksub * d.dsub, 1);
+    bytes[1] = (uint64_t)std::max<int64_t>(d.ntotal * d.code_size, 1);
+    bytes[2] = sizeof(int32_t) * (uint64_t)std::max<int64_t>(d.ntotal * d.deg0, 1);
+    bytes[3] = sizeof(uint32_t) * (uint64_t)std::max<int64_t>(d.ntotal, 1);
+    bytes[4] = sizeof(int32_t) * (uint64_t)std::max<int64_t>(d.upper_len, 1);
+}
+void **index_buffers(drm::DeviceIndex &d, void **out)
+{
+    out[0] = d.centroids;
+    out[1] = d.codes;
+    out[2] = d.nbr0;
+    out[3] = d.upper_off;
+    out[4] = d.upper_nbr;
+    return out;
+}
+} // namespace
+
+extern "C" {
+
+int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_index **out)
+{
+    // every rank of the job runs every collective below in the same order whatever fails locally: a failure before a
+    // data transfer is carried through comm_all_ok, so no rank is left waiting in a broadcast another rank skipped
+    return guarded([&] {
+        if (!comm)
+            throw Error(DRM_ERR_ARG, "drm_index_broadcast: null communicator");
+        const int rank = drm::comm_rank(comm), nranks = drm::comm_nranks(comm), device = drm::comm_device(comm);
+        if (root < 0 || root >= nranks)
+            throw Error(DRM_ERR_ARG, "drm_index_broadcast: root out of range");
+        if (out)
+            *out = nullptr;
+        DRM_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        DRM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        struct StreamGuard {
+            hipStream_t s;
+            ~StreamGuard() { (void)hipStreamDestroy(s); }
+        } sg{s};
+        const bool is_root = rank == root;
+        std::string why;
+        // 1. the root's header (with its buffer checksums)
+        IndexWire w{};
+        if (is_root) {
+            if (!root_index)
+                why = "the root passes its loaded index";
+            else if (root_index->dev.device != device)
+                why = "the root's index lives on device " + std::to_string(root_index->dev.device) +
+                      ", its communicator on device " + std::to_string(device);
+            else {
+                drm::DeviceIndex &r = root_index->dev;
+                w.magic = kBcastMagic;
+                w.d = r.d, w.pq_M = r.pq_M, w.pq_nbits = r.pq_nbits, w.dsub = r.dsub, w.ksub = r.ksub;
+                w.code_size = r.code_size, w.deg0 = r.deg0, w.n_levels = r.n_levels, w.max_level = r.max_level;
+                w.entry_point = r.entry_point, w.has_dup_links = r.has_dup_links;
+                std::memcpy(w.cum, r.cum, sizeof(w.cum));
+                w.ntotal = r.ntotal, w.upper_len = r.upper_len;
+                w.hdr_d = r.meta.hdr.d, w.hdr_metric_type = r.meta.hdr.metric_type, w.hdr_ntotal = r.meta.hdr.ntotal;
+                w.hdr_metric_arg = r.meta.hdr.metric_arg, w.hdr_is_trained = r.meta.hdr.is_trained;
+                w.efConstruction = r.meta.efConstruction, w.efSearch = r.meta.efSearch;
+                w.meta_pq_M = r.meta.pq_M, w.meta_pq_nbits = r.meta.pq_nbits;
+                index_buffer_sizes(r, w.bytes);
+                void *bufs[kBcastBufs];
+                index_buffers(r, bufs);
+                for (int b = 0; b < kBcastBufs; ++b)
+                    w.sums[b] = device_checksum(bufs[b], (int64_t)w.bytes[b], s);
+            }
+        } else if (!out) {
+            why = "a receiving rank passes `out`";
+        }
+        if (!drm::comm_all_ok(comm, why.empty(), s))
+            throw Error(DRM_ERR_ARG, "drm_index_broadcast: " + (why.empty() ? std::string("another rank's arguments were refused") : why));
+        {
+            DevBuf<uint8_t> dw(sizeof(IndexWire));
+            if (is_root)
+                dw.upload(reinterpret_cast<const uint8_t *>(&w));
+            const drm::BcastItem hdr{dw.p, dw.p, sizeof(IndexWire)};
+            drm::comm_broadcast(comm, &hdr, 1, root, s);
+            dw.download(reinterpret_cast<uint8_t *>(&w));
+        }
+        // 2. the receiver's index (a root asking for a copy receives too)
+        std::unique_ptr<drm_index> ix;
+        const bool receive = out != nullptr;
+        if (receive) {
+            try {
+                uint64_t expect[kBcastBufs];
+                drm::DeviceIndex probe;
+                probe.pq_M = w.pq_M, probe.ksub = w.ksub, probe.dsub = w.dsub, probe.ntotal = w.ntotal;
+                probe.code_size = w.code_size, probe.deg0 = w.deg0, probe.upper_len = w.upper_len;
+                if (w.magic != kBcastMagic || w.ntotal <= 0 || w.deg0 < 1 || w.n_levels < 1 ||
+                    w.n_levels > drm::kMaxLevels || w.upper_len < 0 || w.pq_M < 1 || w.ksub < 1 || w.dsub < 1)
+                    throw Error(DRM_ERR_FORMAT, "malformed index header");
+                index_buffer_sizes(probe, expect);
+                if (std::memcmp(expect, w.bytes, sizeof(expect)) != 0)
+                    throw Error(DRM_ERR_FORMAT, "index header sizes disagree");
+                ix.reset(new drm_index());
+                drm::DeviceIndex &d = ix->dev;
+                d.device = device;
+                d.d = w.d, d.pq_M = w.pq_M, d.pq_nbits = w.pq_nbits, d.dsub = w.dsub, d.ksub = w.ksub;
+                d.code_size = w.code_size, d.deg0 = w.deg0, d.n_levels = w.n_levels, d.max_level = w.max_level;
+                d.entry_point = w.entry_point, d.has_dup_links = w.has_dup_links;
+                std::memcpy(d.cum, w.cum, sizeof(d.cum));
+                d.ntotal = w.ntotal, d.upper_len = w.upper_len;
+                d.meta.hdr.d = w.hdr_d, d.meta.hdr.metric_type = w.hdr_metric_type, d.meta.hdr.ntotal = w.hdr_ntotal;
+                d.meta.hdr.metric_arg = w.hdr_metric_arg, d.meta.hdr.is_trained = (uint8_t)w.hdr_is_trained;
+                d.meta.efConstruction = w.efConstruction, d.meta.efSearch = w.efSearch;
+                d.meta.entry_point = w.entry_point, d.meta.max_level = w.max_level;
+                d.meta.pq_M = w.meta_pq_M, d.meta.pq_nbits = w.meta_pq_nbits;
+                d.meta.cum_nneighbor_per_level.assign(w.cum, w.cum + w.n_levels + 1);
+                apply_load_env(d);
+                void **slots[kBcastBufs] = {(void **)&d.centroids, (void **)&d.codes, (void **)&d.nbr0,
+                                            (void **)&d.upper_off, (void **)&d.upper_nbr};
+                for (int b = 0; b < kBcastBufs; ++b) {
+                    DRM_HIP_CHECK(drm::malloc_big(slots[b], w.bytes[b], drm::kBigIndex));
+                    d.device_bytes += (int64_t)w.bytes[b];
+                }
+            } catch (const std::exception &e) {
+                why = e.what();
+                if (ix)
+                    free_index(ix->dev);
+                ix.reset();
+            }
+        }
+        if (!drm::comm_all_ok(comm, why.empty(), s))
+            throw Error(DRM_ERR_HIP, "drm_index_broadcast: " + (why.empty() ? std::string("another rank could not take the index") : why));
+        // 3. the buffers, in one grouped broadcast; each receiver checks what arrived against the root's checksums
+        //    and derives the lean kernel's inline rows locally (they are a function of nbr0 + codes)
+        drm::BcastItem items[kBcastBufs];
+        void *src[kBcastBufs] = {};
+        if (is_root)
+            index_buffers(root_index->dev, src);
+        void *dst[kBcastBufs] = {};
+        if (receive)
+            index_buffers(ix->dev, dst);
+        for (int b = 0; b < kBcastBufs; ++b)
+            items[b] = drm::BcastItem{src[b], receive ? dst[b] : src[b], (size_t)w.bytes[b]};
+        try {
+            drm::comm_broadcast(comm, items, kBcastBufs, root, s);
+        } catch (...) {
+            if (ix)
+                free_index(ix->dev);
+            throw;
+        }
+        if (receive) {
+            try {
+                for (int b = 0; b < kBcastBufs; ++b) {
+                    const uint64_t got = device_checksum(dst[b], (int64_t)w.bytes[b], s);
+                    if (got != w.sums[b]) {
+                        char msg[160];
+                        std::snprintf(msg, sizeof msg, "buffer %d (%llu bytes) arrived with checksum %016llx, the root's is "
+                                      "%016llx", b, (unsigned long long)w.bytes[b], (unsigned long long)got,
+                                      (unsigned long long)w.sums[b]);
+                        throw Error(DRM_ERR_INTERNAL, msg);
+                    }
+                }
+                drm::DeviceIndex &d = ix->dev;
+                if (d.use_inline)
+                    drm::build_inline_rows(d);
+                drm::reserve_search_scratch(d);
+            } catch (const std::exception &e) {
+                why = e.what();
+                free_index(ix->dev);
+                ix.reset();
+            }
+        }
+        if (!drm::comm_all_ok(comm, why.empty(), s)) {
+            if (ix)
+                free_index(ix->dev);
+            throw Error(DRM_ERR_INTERNAL, "drm_index_broadcast: " + (why.empty() ? std::string("another rank failed to verify the index") : why));
+        }
+        if (receive)
+            *out = ix.release();
     });
 }
 

@@ -18,6 +18,21 @@ struct Error : std::runtime_error {
 
 void set_last_error(const std::string &msg);
 
+// RCCL helpers over a drm_comm (exec.cpp), for collectives the C ABI builds on (drm_index_broadcast, capi.cpp):
+// a grouped ncclBroadcast of byte ranges from `root` (send is read on the root only; recv may equal send there),
+// synchronised on `stream`; and an agreement step (min over ranks of `ok`) that every rank reaches before a
+// collective that a failed rank would not enter
+struct BcastItem {
+    const void *send;
+    void *recv;
+    size_t bytes;
+};
+int comm_rank(const drm_comm *c);
+int comm_nranks(const drm_comm *c);
+int comm_device(const drm_comm *c);
+void comm_broadcast(drm_comm *c, const BcastItem *items, int n, int root, void *stream); // throws Error
+int comm_all_ok(drm_comm *c, bool ok, void *stream);                                   // throws Error
+
 // ---------------------------------------------------------------------------------------------
 // Host image of a faiss IndexHNSWPQ: exactly the fields faiss::write_index / read_index touch
 // for fourcc "IHNp" + storage "IxPq" [faiss impl/index_write.cpp, impl/index_read.cpp].

@@ -723,6 +723,41 @@ void nccl_check(ncclResult_t r, const char *what)
 }
 } // namespace
 
+namespace drm {
+int comm_rank(const drm_comm *c) { return c->rank; }
+int comm_nranks(const drm_comm *c) { return c->nranks; }
+int comm_device(const drm_comm *c) { return c->device; }
+
+void comm_broadcast(drm_comm *c, const BcastItem *items, int n, int root, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    HC(hipSetDevice(c->device));
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int i = 0; i < n; ++i)
+        if (items[i].bytes > 0)
+            nccl_check(ncclBroadcast(c->rank == root ? items[i].send : nullptr, items[i].recv, items[i].bytes, ncclUint8,
+                                     root, c->comm, s),
+                       "ncclBroadcast");
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    HC(hipStreamSynchronize(s));
+}
+
+int comm_all_ok(drm_comm *c, bool ok, void *stream)
+{
+    // plain allocation and synchronous copies around the one collective (see device_checksum, capi.cpp)
+    hipStream_t s = (hipStream_t)stream;
+    HC(hipSetDevice(c->device));
+    DevMem d(sizeof(int32_t));
+    const int32_t h = ok ? 1 : 0;
+    HC(hipMemcpy(d.p, &h, sizeof(h), hipMemcpyHostToDevice));
+    nccl_check(ncclAllReduce(d.p, d.p, 1, ncclInt32, ncclMin, c->comm, s), "ncclAllReduce");
+    HC(hipStreamSynchronize(s));
+    int32_t r = 0;
+    HC(hipMemcpy(&r, d.p, sizeof(r), hipMemcpyDeviceToHost));
+    return r;
+}
+} // namespace drm
+
 extern "C" {
 
 int drm_comm_unique_id(uint8_t *id)

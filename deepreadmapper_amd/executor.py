@@ -169,6 +169,12 @@ class Comm:
         self._h = h.value
         self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
 
+    @property
+    def handle(self):
+        if not self._h:
+            raise RuntimeError("communicator was freed")
+        return self._h
+
     def gather_rows(self, d_send, n_total, row_bytes, d_recv=None, root=0, stream=None):
         """Rows [r*n/G, (r+1)*n/G) of every rank's d_send (DeviceBuffer) land in the root's d_recv."""
         check(lib().drm_comm_gather_rows(self._h, d_send.ptr, int(n_total), int(row_bytes),

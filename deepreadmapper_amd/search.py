@@ -18,13 +18,31 @@ class HnswPqIndex:
     def __init__(self, path, device=0):
         h = C.c_void_p()
         check(lib().drm_index_load(str(path).encode(), int(device), C.byref(h)))
-        self._h = h.value
+        self._adopt(h.value, device)
+
+    def _adopt(self, handle, device):
+        self._h = handle
         self.device = int(device)
         info = IndexInfo()
         check(lib().drm_index_get_info(self._h, C.byref(info)))
         self.info = info
         self.d = info.d
         self.ntotal = info.ntotal
+
+    @classmethod
+    def broadcast(cls, comm, index=None, root=0, copy=False):
+        """drm_index_broadcast: collective over `comm` (executor.Comm). The root passes its loaded index and gets it
+        back (or, with copy=True, a separate replica received through the same path); every other rank passes None
+        and gets a new replica on the communicator's device, received over RCCL instead of parsed from the file."""
+        h = C.c_void_p()
+        want = comm.rank != root or copy
+        check(lib().drm_index_broadcast(comm.handle, index.handle if index is not None else None, int(root),
+                                        C.byref(h) if want else None))
+        if not want:
+            return index
+        obj = cls.__new__(cls)
+        obj._adopt(h.value, comm.device)
+        return obj
 
     @property
     def handle(self):

@@ -361,6 +361,17 @@ int drm_comm_init(const uint8_t *id, int nranks, int rank, int device, drm_comm 
 int drm_comm_free(drm_comm *comm);
 int drm_comm_gather_rows(drm_comm *comm, const void *d_send, int64_t n_total, int64_t row_bytes, void *d_recv, int root,
                          void *stream);
+/* drm_index_broadcast: the index replicated from one GPU to every rank over RCCL ("index
+ * broadcast from GPU0"), in place of every rank parsing the IHNp file (drm_index_load; src/main.cpp:236-237 is
+ * the load it replaces on ranks != root). Collective: every rank of `comm` calls it, on the communicator's device.
+ * The root passes its loaded index in root_index (other ranks pass NULL); every other rank receives a new index in
+ * *out. At the root `out` may be NULL (its index is the replica) or non-NULL for a separate copy (what a
+ * one-rank job uses to exercise the receive side). The header goes first (shape, levels, entry point, kept
+ * metadata, and the root's checksum of each buffer), then the PQ centroids, codes, level-0 rows and upper-level
+ * lists in one grouped ncclBroadcast; each receiver checks the checksums, derives the lean kernel's inline rows
+ * itself and applies its own DRM_SEARCH_* load-time knobs. An argument, allocation or checksum failure on any rank
+ * fails the call on every rank (an agreement step precedes each transfer, so none is left waiting). Synchronous. */
+int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_index **out);
 
 /* post_process_sw_dynamic (src/utils/post_processor.cpp:357-452) on a genome handle: the same
  * contract as drm_post_process_sw_static, with find_sequences' dynamic candidate rules (dense: every

@@ -151,6 +151,80 @@ def test_bench_gather_checksums_every_rank(tmp_path, shift, expect):
     assert json.load(open(f"{out}.0"))["match"][1] == expect  # (shift -1 also overwrites rank 0's last row)
 
 
+def _replica_worker(rank, world, port, mode, out_path):
+    """One rank of a gloo job running bench.load_index with the GPU pieces stood in: two devices, a communicator
+    that only records itself, an index class whose file load and RCCL broadcast are tagged (the broadcast fails on
+    rank 1 when mode == "fail")."""
+    import json
+    import sys
+    import types
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    import deepreadmapper_amd.device as dev_mod
+    import deepreadmapper_amd.executor as ex_mod
+    import deepreadmapper_amd.search as se_mod
+    dev_mod.device_count = lambda: 2
+    events = []
+
+    class FakeComm:
+        @staticmethod
+        def unique_id():
+            return b"u" * 128
+
+        def __init__(self, uid, nranks, rank_, device):
+            assert uid == b"u" * 128 and nranks == world and rank_ == rank
+            self.rank, self.device = rank_, device
+
+        def free(self):
+            pass
+
+    class FakeIndex:
+        def __init__(self, path, device, how="file"):
+            self.how, self.info = how, types.SimpleNamespace(device_bytes=123)
+            events.append(how)
+
+        @classmethod
+        def broadcast(cls, comm, index, root=0, copy=False):
+            assert (index is not None) == (comm.rank == root)
+            if mode == "fail" and comm.rank == 1:
+                raise RuntimeError("forced")
+            return index if comm.rank == root else cls(None, comm.device, how="bcast")
+
+        def free(self):
+            events.append("free")
+
+    ex_mod.Comm, se_mod.HnswPqIndex = FakeComm, FakeIndex
+    D = bench.Dist()
+    args = types.SimpleNamespace(index_bcast=mode != "off")
+    ix, info = bench.load_index(args, D, "x.index", rank)
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump({"mode": info["mode"], "why": info.get("why"), "how": ix.how, "events": events}, f)
+    D.close()
+
+
+@pytest.mark.parametrize("mode", ["ok", "fail", "off"])
+def test_bench_index_replication_two_ranks(tmp_path, mode):
+    """bench.py at N > 1: rank 0 loads the index file and the others receive it by drm_index_broadcast; a broadcast
+    failing on any rank (here rank 1 only) sends every rank back to loading the file itself, and the JSON line says
+    so; --no-index-bcast loads the file on every rank."""
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "r")
+    mp.spawn(_replica_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
+    got = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    if mode == "ok":
+        assert [g["mode"] for g in got] == ["rccl broadcast (drm_index_broadcast)"] * 2
+        assert got[0]["events"] == ["file"] and got[1]["events"] == ["bcast"]
+        assert got[0]["how"] == "file" and got[1]["how"] == "bcast"
+    else:
+        assert all(g["mode"] == "file per rank" and g["how"] == "file" for g in got)
+        assert got[0]["why"] == ("broadcast failed" if mode == "fail" else "--no-index-bcast")
+        if mode == "fail":  # rank 0 dropped its loaded replica and loaded again with everyone
+            assert got[0]["events"] == ["file", "free", "file"] and got[1]["events"] == ["file"]
+
+
 def test_host_checksum_properties():
     """drm_device_checksum's host form: position-dependent (swapped words, a shifted row, a changed byte in the
     zero-padded tail all change it), and the empty buffer sums to 0."""

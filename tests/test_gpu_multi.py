@@ -102,6 +102,47 @@ def test_rccl_gather_one_rank():
     c.free()
 
 
+def test_index_broadcast_one_rank_copy(syn20k):
+    """drm_index_broadcast's receive side on a one-rank job (copy=True: the root receives a separate replica through
+    the header, agreement, grouped ncclBroadcast and checksum steps): the replica searches bit-identically to the
+    loaded index (ids, 0-ulp distances, ndis, nhops) and reports the same header."""
+    from deepreadmapper_amd import read_index
+    from deepreadmapper_amd.executor import Comm
+    from deepreadmapper_amd.search import HnswPqIndex
+    w = syn20k["w"]
+    c = Comm(Comm.unique_id(), 1, 0, 0)
+    ix = read_index(w.index_path)
+    same = HnswPqIndex.broadcast(c, ix, root=0)  # the root's own index is the replica
+    assert same is ix
+    rep = HnswPqIndex.broadcast(c, ix, root=0, copy=True)
+    assert rep.handle != ix.handle
+    for f in ("d", "ntotal", "pq_M", "pq_nbits", "M_hnsw", "max_level", "entry_point", "efConstruction", "efSearch",
+              "metric_type", "device_bytes"):
+        assert getattr(rep.info, f) == getattr(ix.info, f), f
+    q = w.q_emb[:1000]
+    D0, I0, s0 = ix.search(q, 128, 128)
+    ix.free()  # the replica owns its buffers
+    D1, I1, s1 = rep.search(q, 128, 128)
+    assert np.array_equal(I0, I1) and np.array_equal(D0.view(np.uint32), D1.view(np.uint32))
+    assert (s0.ndis, s0.nhops) == (s1.ndis, s1.nhops)
+    rep.free()
+    c.free()
+
+
+def test_index_broadcast_argument_errors(syn20k):
+    from deepreadmapper_amd._native import DrmError, DRM_ERR_ARG
+    from deepreadmapper_amd.executor import Comm
+    from deepreadmapper_amd.search import HnswPqIndex
+    c = Comm(Comm.unique_id(), 1, 0, 0)
+    with pytest.raises(DrmError) as e:  # the root without an index: refused on every rank before any transfer
+        HnswPqIndex.broadcast(c, None, root=0, copy=True)
+    assert e.value.code == DRM_ERR_ARG
+    with pytest.raises(DrmError) as e:
+        HnswPqIndex.broadcast(c, None, root=1)
+    assert e.value.code == DRM_ERR_ARG
+    c.free()
+
+
 def test_pipeline_cli_multi_devices(tmp_path):
     fna = os.path.join(GOLDEN, "ecoli_150.fna")
     fq = os.path.join(GOLDEN, "test_data.fastq")
