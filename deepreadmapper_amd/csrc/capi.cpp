@@ -418,6 +418,84 @@ void **index_buffers(drm::DeviceIndex &d, void **out)
     out[4] = d.upper_nbr;
     return out;
 }
+
+// the header of an index (no checksums)
+IndexWire index_to_wire(const drm::DeviceIndex &r)
+{
+    IndexWire w{};
+    w.magic = kBcastMagic;
+    w.d = r.d, w.pq_M = r.pq_M, w.pq_nbits = r.pq_nbits, w.dsub = r.dsub, w.ksub = r.ksub;
+    w.code_size = r.code_size, w.deg0 = r.deg0, w.n_levels = r.n_levels, w.max_level = r.max_level;
+    w.entry_point = r.entry_point, w.has_dup_links = r.has_dup_links;
+    std::memcpy(w.cum, r.cum, sizeof(w.cum));
+    w.ntotal = r.ntotal, w.upper_len = r.upper_len;
+    w.hdr_d = r.meta.hdr.d, w.hdr_metric_type = r.meta.hdr.metric_type, w.hdr_ntotal = r.meta.hdr.ntotal;
+    w.hdr_metric_arg = r.meta.hdr.metric_arg, w.hdr_is_trained = r.meta.hdr.is_trained;
+    w.efConstruction = r.meta.efConstruction, w.efSearch = r.meta.efSearch;
+    w.meta_pq_M = r.meta.pq_M, w.meta_pq_nbits = r.meta.pq_nbits;
+    index_buffer_sizes(r, w.bytes);
+    return w;
+}
+
+// a new index on `device` from a header: validated, the load-time knobs applied, its five buffers allocated (not
+// filled); throws Error
+std::unique_ptr<drm_index> index_from_wire(const IndexWire &w, int device)
+{
+    uint64_t expect[kBcastBufs];
+    drm::DeviceIndex probe;
+    probe.pq_M = w.pq_M, probe.ksub = w.ksub, probe.dsub = w.dsub, probe.ntotal = w.ntotal;
+    probe.code_size = w.code_size, probe.deg0 = w.deg0, probe.upper_len = w.upper_len;
+    if (w.magic != kBcastMagic || w.ntotal <= 0 || w.deg0 < 1 || w.n_levels < 1 || w.n_levels > drm::kMaxLevels ||
+        w.upper_len < 0 || w.pq_M < 1 || w.ksub < 1 || w.dsub < 1)
+        throw Error(DRM_ERR_FORMAT, "malformed index header");
+    index_buffer_sizes(probe, expect);
+    if (std::memcmp(expect, w.bytes, sizeof(expect)) != 0)
+        throw Error(DRM_ERR_FORMAT, "index header sizes disagree");
+    DRM_HIP_CHECK(hipSetDevice(device));
+    std::unique_ptr<drm_index> ix(new drm_index());
+    drm::DeviceIndex &d = ix->dev;
+    d.device = device;
+    d.d = w.d, d.pq_M = w.pq_M, d.pq_nbits = w.pq_nbits, d.dsub = w.dsub, d.ksub = w.ksub;
+    d.code_size = w.code_size, d.deg0 = w.deg0, d.n_levels = w.n_levels, d.max_level = w.max_level;
+    d.entry_point = w.entry_point, d.has_dup_links = w.has_dup_links;
+    std::memcpy(d.cum, w.cum, sizeof(d.cum));
+    d.ntotal = w.ntotal, d.upper_len = w.upper_len;
+    d.meta.hdr.d = w.hdr_d, d.meta.hdr.metric_type = w.hdr_metric_type, d.meta.hdr.ntotal = w.hdr_ntotal;
+    d.meta.hdr.metric_arg = w.hdr_metric_arg, d.meta.hdr.is_trained = (uint8_t)w.hdr_is_trained;
+    d.meta.efConstruction = w.efConstruction, d.meta.efSearch = w.efSearch;
+    d.meta.entry_point = w.entry_point, d.meta.max_level = w.max_level;
+    d.meta.pq_M = w.meta_pq_M, d.meta.pq_nbits = w.meta_pq_nbits;
+    d.meta.cum_nneighbor_per_level.assign(w.cum, w.cum + w.n_levels + 1);
+    try {
+        apply_load_env(d);
+        void **slots[kBcastBufs] = {(void **)&d.centroids, (void **)&d.codes, (void **)&d.nbr0, (void **)&d.upper_off,
+                                    (void **)&d.upper_nbr};
+        for (int b = 0; b < kBcastBufs; ++b) {
+            DRM_HIP_CHECK(drm::malloc_big(slots[b], w.bytes[b], drm::kBigIndex));
+            d.device_bytes += (int64_t)w.bytes[b];
+        }
+    } catch (...) {
+        free_index(d);
+        throw;
+    }
+    return ix;
+}
+
+// after the five buffers are filled: the lean kernel's inline rows (a function of nbr0 + codes) and the search
+// scratch, as drm_index_load makes them; frees the index and rethrows on failure
+void index_finish(drm_index *ix)
+{
+    try {
+        drm::DeviceIndex &d = ix->dev;
+        DRM_HIP_CHECK(hipSetDevice(d.device));
+        if (d.use_inline)
+            drm::build_inline_rows(d);
+        drm::reserve_search_scratch(d);
+    } catch (...) {
+        free_index(ix->dev);
+        throw;
+    }
+}
 } // namespace
 
 extern "C" {
@@ -453,17 +531,7 @@ int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_ind
                       ", its communicator on device " + std::to_string(device);
             else {
                 drm::DeviceIndex &r = root_index->dev;
-                w.magic = kBcastMagic;
-                w.d = r.d, w.pq_M = r.pq_M, w.pq_nbits = r.pq_nbits, w.dsub = r.dsub, w.ksub = r.ksub;
-                w.code_size = r.code_size, w.deg0 = r.deg0, w.n_levels = r.n_levels, w.max_level = r.max_level;
-                w.entry_point = r.entry_point, w.has_dup_links = r.has_dup_links;
-                std::memcpy(w.cum, r.cum, sizeof(w.cum));
-                w.ntotal = r.ntotal, w.upper_len = r.upper_len;
-                w.hdr_d = r.meta.hdr.d, w.hdr_metric_type = r.meta.hdr.metric_type, w.hdr_ntotal = r.meta.hdr.ntotal;
-                w.hdr_metric_arg = r.meta.hdr.metric_arg, w.hdr_is_trained = r.meta.hdr.is_trained;
-                w.efConstruction = r.meta.efConstruction, w.efSearch = r.meta.efSearch;
-                w.meta_pq_M = r.meta.pq_M, w.meta_pq_nbits = r.meta.pq_nbits;
-                index_buffer_sizes(r, w.bytes);
+                w = index_to_wire(r);
                 void *bufs[kBcastBufs];
                 index_buffers(r, bufs);
                 for (int b = 0; b < kBcastBufs; ++b)
@@ -487,46 +555,16 @@ int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_ind
         const bool receive = out != nullptr;
         if (receive) {
             try {
-                uint64_t expect[kBcastBufs];
-                drm::DeviceIndex probe;
-                probe.pq_M = w.pq_M, probe.ksub = w.ksub, probe.dsub = w.dsub, probe.ntotal = w.ntotal;
-                probe.code_size = w.code_size, probe.deg0 = w.deg0, probe.upper_len = w.upper_len;
-                if (w.magic != kBcastMagic || w.ntotal <= 0 || w.deg0 < 1 || w.n_levels < 1 ||
-                    w.n_levels > drm::kMaxLevels || w.upper_len < 0 || w.pq_M < 1 || w.ksub < 1 || w.dsub < 1)
-                    throw Error(DRM_ERR_FORMAT, "malformed index header");
-                index_buffer_sizes(probe, expect);
-                if (std::memcmp(expect, w.bytes, sizeof(expect)) != 0)
-                    throw Error(DRM_ERR_FORMAT, "index header sizes disagree");
-                ix.reset(new drm_index());
-                drm::DeviceIndex &d = ix->dev;
-                d.device = device;
-                d.d = w.d, d.pq_M = w.pq_M, d.pq_nbits = w.pq_nbits, d.dsub = w.dsub, d.ksub = w.ksub;
-                d.code_size = w.code_size, d.deg0 = w.deg0, d.n_levels = w.n_levels, d.max_level = w.max_level;
-                d.entry_point = w.entry_point, d.has_dup_links = w.has_dup_links;
-                std::memcpy(d.cum, w.cum, sizeof(d.cum));
-                d.ntotal = w.ntotal, d.upper_len = w.upper_len;
-                d.meta.hdr.d = w.hdr_d, d.meta.hdr.metric_type = w.hdr_metric_type, d.meta.hdr.ntotal = w.hdr_ntotal;
-                d.meta.hdr.metric_arg = w.hdr_metric_arg, d.meta.hdr.is_trained = (uint8_t)w.hdr_is_trained;
-                d.meta.efConstruction = w.efConstruction, d.meta.efSearch = w.efSearch;
-                d.meta.entry_point = w.entry_point, d.meta.max_level = w.max_level;
-                d.meta.pq_M = w.meta_pq_M, d.meta.pq_nbits = w.meta_pq_nbits;
-                d.meta.cum_nneighbor_per_level.assign(w.cum, w.cum + w.n_levels + 1);
-                apply_load_env(d);
-                void **slots[kBcastBufs] = {(void **)&d.centroids, (void **)&d.codes, (void **)&d.nbr0,
-                                            (void **)&d.upper_off, (void **)&d.upper_nbr};
-                for (int b = 0; b < kBcastBufs; ++b) {
-                    DRM_HIP_CHECK(drm::malloc_big(slots[b], w.bytes[b], drm::kBigIndex));
-                    d.device_bytes += (int64_t)w.bytes[b];
-                }
+                ix = index_from_wire(w, device);
             } catch (const std::exception &e) {
                 why = e.what();
-                if (ix)
-                    free_index(ix->dev);
-                ix.reset();
             }
         }
-        if (!drm::comm_all_ok(comm, why.empty(), s))
+        if (!drm::comm_all_ok(comm, why.empty(), s)) {
+            if (ix)
+                free_index(ix->dev);
             throw Error(DRM_ERR_HIP, "drm_index_broadcast: " + (why.empty() ? std::string("another rank could not take the index") : why));
+        }
         // 3. the buffers, in one grouped broadcast; each receiver checks what arrived against the root's checksums
         //    and derives the lean kernel's inline rows locally (they are a function of nbr0 + codes)
         drm::BcastItem items[kBcastBufs];
@@ -557,14 +595,18 @@ int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_ind
                         throw Error(DRM_ERR_INTERNAL, msg);
                     }
                 }
-                drm::DeviceIndex &d = ix->dev;
-                if (d.use_inline)
-                    drm::build_inline_rows(d);
-                drm::reserve_search_scratch(d);
             } catch (const std::exception &e) {
                 why = e.what();
                 free_index(ix->dev);
                 ix.reset();
+            }
+            if (ix) {
+                try {
+                    index_finish(ix.get());
+                } catch (const std::exception &e) {
+                    why = e.what();
+                    ix.reset(); // index_finish freed its buffers
+                }
             }
         }
         if (!drm::comm_all_ok(comm, why.empty(), s)) {
@@ -574,6 +616,35 @@ int drm_index_broadcast(drm_comm *comm, drm_index *root_index, int root, drm_ind
         }
         if (receive)
             *out = ix.release();
+    });
+}
+
+int drm_index_clone(const drm_index *src, int device, drm_index **out)
+{
+    return guarded([&] {
+        if (!src || !out)
+            throw Error(DRM_ERR_ARG, "null argument");
+        *out = nullptr;
+        drm::DeviceIndex &r = const_cast<drm_index *>(src)->dev;
+        const IndexWire w = index_to_wire(r);
+        std::unique_ptr<drm_index> ix = index_from_wire(w, device);
+        void *from[kBcastBufs], *to[kBcastBufs];
+        index_buffers(r, from);
+        index_buffers(ix->dev, to);
+        try {
+            // device to device (peer copies over xGMI when the devices differ; the runtime stages them if peer
+            // access is off), from the source's device
+            DRM_HIP_CHECK(hipSetDevice(r.device));
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+            for (int b = 0; b < kBcastBufs; ++b)
+                DRM_HIP_CHECK(hipMemcpyPeer(to[b], device, from[b], r.device, w.bytes[b]));
+            DRM_HIP_CHECK(hipDeviceSynchronize());
+        } catch (...) {
+            free_index(ix->dev);
+            throw;
+        }
+        index_finish(ix.get());
+        *out = ix.release();
     });
 }
 

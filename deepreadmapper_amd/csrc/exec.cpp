@@ -601,6 +601,24 @@ void free_multi(drm_multi *m)
 
 extern "C" {
 
+} // extern "C"
+
+namespace {
+// the index replicas of a drm_multi: the file parsed once, on the first device, and cloned device to device to
+// the others (drm_index_clone), in parallel -- not one host parse and one host image per device
+void load_replicas(const char *index_path, drm_multi *m)
+{
+    const int ndev = (int)m->devices.size();
+    abi_check(drm_index_load(index_path, m->devices[0], &m->index[0]));
+    if (ndev > 1)
+        fan_out(ndev - 1, [&](int r) {
+            abi_check(drm_index_clone(m->index[0], m->devices[(size_t)r + 1], &m->index[(size_t)r + 1]));
+        });
+}
+} // namespace
+
+extern "C" {
+
 int drm_multi_create(const char *index_path, const int *devices, int ndev, const uint8_t *windows, int64_t n_ref,
                      int32_t ref_len, int64_t row_stride, drm_multi **out)
 {
@@ -613,8 +631,8 @@ int drm_multi_create(const char *index_path, const int *devices, int ndev, const
         m->index.assign((size_t)ndev, nullptr);
         m->refs.assign((size_t)ndev, nullptr);
         try {
+            load_replicas(index_path, m.get());
             fan_out(ndev, [&](int r) {
-                abi_check(drm_index_load(index_path, m->devices[(size_t)r], &m->index[(size_t)r]));
                 if (windows)
                     abi_check(drm_refs_create(windows, n_ref, ref_len, row_stride, m->devices[(size_t)r],
                                               &m->refs[(size_t)r]));
@@ -639,8 +657,8 @@ int drm_multi_create_genome(const char *index_path, const int *devices, int ndev
         m->index.assign((size_t)ndev, nullptr);
         m->refs.assign((size_t)ndev, nullptr);
         try {
+            load_replicas(index_path, m.get());
             fan_out(ndev, [&](int r) {
-                abi_check(drm_index_load(index_path, m->devices[(size_t)r], &m->index[(size_t)r]));
                 abi_check(drm_refs_create_genome(genome, len, ref_len, m->devices[(size_t)r], &m->refs[(size_t)r]));
             });
         } catch (...) {

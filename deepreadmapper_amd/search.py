@@ -44,6 +44,15 @@ class HnswPqIndex:
         obj._adopt(h.value, comm.device)
         return obj
 
+    def clone(self, device=None):
+        """drm_index_clone: a replica on `device` (default: this index's device), copied device to device."""
+        device = self.device if device is None else int(device)
+        h = C.c_void_p()
+        check(lib().drm_index_clone(self.handle, device, C.byref(h)))
+        obj = type(self).__new__(type(self))
+        obj._adopt(h.value, device)
+        return obj
+
     @property
     def handle(self):
         if not self._h:

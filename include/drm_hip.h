@@ -100,6 +100,10 @@ int drm_event_elapsed_ms(void *start, void *stop, float *ms);
  * `device`. drm_index_free replaces `delete alg_hnsw` (src/main.cpp:299). */
 int drm_index_load(const char *path, int device, drm_index **out);
 int drm_index_free(drm_index *index);
+/* drm_index_clone: a replica of a loaded index on `device` (device-to-device copies of its buffers, over xGMI
+ * between GPUs, the inline rows derived on the target), for one process driving several GPUs: the file is parsed
+ * once (drm_multi_create does this). The source is not changed. */
+int drm_index_clone(const drm_index *src, int device, drm_index **out);
 int drm_index_get_info(const drm_index *index, drm_index_info *info);
 
 /* drm_search replaces faiss_search(index, query_data, k, ef) (includes/hnswpq/search.hpp:18-21,

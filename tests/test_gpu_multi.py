@@ -2,8 +2,9 @@
 
 * drm_search_rerank (batched, three streams, ping-pong device buffers) equals drm_search followed by
   drm_post_process_sw_static bit for bit, for one batch and for many uneven batches;
-* drm_multi_search_rerank over G replicas -- here G "logical devices" that all map to device 0 of the
-  one-GPU box -- writes outputs byte-identical to the one-device run (contiguous shards, no exchange);
+* drm_multi_search_rerank over G replicas (the file parsed once, the others drm_index_clone copies) -- here
+  G "logical devices" that all map to device 0 of the one-GPU box -- writes outputs byte-identical to the
+  one-device run (contiguous shards, no exchange);
 * the RCCL gather (drm_comm_gather_rows) of a one-rank job returns the rank's rows;
 * bin/pipeline with DRM_DEVICES=0,0,0 writes the same .npy files as with one device.
 Reference call sites: src/main.cpp:278 (faiss_search), :333-341 (post_process_sw_static), the OpenMP
@@ -127,6 +128,23 @@ def test_index_broadcast_one_rank_copy(syn20k):
     assert (s0.ndis, s0.nhops) == (s1.ndis, s1.nhops)
     rep.free()
     c.free()
+
+
+def test_index_clone_searches_identically(syn20k):
+    """drm_index_clone (what drm_multi_create uses for every device after the first): the clone searches
+    bit-identically and survives the source being freed."""
+    from deepreadmapper_amd import read_index
+    w = syn20k["w"]
+    ix = read_index(w.index_path)
+    cl = ix.clone()
+    assert cl.handle != ix.handle and cl.info.device_bytes == ix.info.device_bytes
+    q = w.q_emb[:1000]
+    D0, I0, s0 = ix.search(q, 64, 128)
+    ix.free()
+    D1, I1, s1 = cl.search(q, 64, 128)
+    assert np.array_equal(I0, I1) and np.array_equal(D0.view(np.uint32), D1.view(np.uint32))
+    assert (s0.ndis, s0.nhops) == (s1.ndis, s1.nhops)
+    cl.free()
 
 
 def test_index_broadcast_argument_errors(syn20k):
