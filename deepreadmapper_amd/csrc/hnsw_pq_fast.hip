@@ -846,8 +846,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
                 // the valid slots' keys: pop_min's, less the slot it just popped
                 const uint32_t hL = popL ? 0xFFFFFFFFu : cL;
                 const uint32_t hR = popR ? 0xFFFFFFFFu : cR;
-                uint32_t mk = dp < hL ? dp : hL;
-                mk = mk < hR ? mk : hR;
+                // one v_min3 (the compiler folds popR's select past the first min and then needs two mins + a select)
+                uint32_t mk;
+                asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mk) : "v"(dp), "v"(hL), "v"(hR));
                 const int32_t hid = hL == mk ? unpack_id(hp.L) : unpack_id(hp.R);
                 const int32_t mid = dp == mk ? v1 : hid;
                 const uint32_t mm = wave_min_u32(mk);

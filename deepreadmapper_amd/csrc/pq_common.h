@@ -70,10 +70,13 @@ __device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v, int ctrl, 
 // min over the 64 lanes, returned wave-uniform
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x111, 0xF));
-    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x112, 0xF));
-    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x114, 0xF));
-    v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x118, 0xF));
+    // row rotations (row_ror:1/2/4/8) first: every lane of a row reads a valid lane (bound_ctrl's zero-fill never
+    // applies), so no identity "old" value -- and no v_mov to initialise one -- is needed, and each stage is one
+    // v_min_u32_dpp; after them every lane holds its row's minimum
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true));
     v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x142, 0xA));
     v = min(v, dpp_u32(0xFFFFFFFFu, v, 0x143, 0xC));
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
