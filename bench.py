@@ -33,8 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# dependent-load latency of the search's pointer chase (a random 384-B row behind a random 384-B row), measured by
-# tools/microbench/memlat.hip on an MI355X box (profiles/r03/box_diag_A.txt); the latency floor of roofline uses it
+# dependent-load latency of the search's pointer chase, measured by tools/microbench/memlat.hip on an MI355X box
+# (profiles/r03/box_diag_A.txt): the fallback when the live probe (dep_load_latency) cannot run
 DEP_LOAD_LATENCY_S = 1.08e-6
 SEARCH_LUT_BYTES = 8 * 256 * 4  # the lean search kernel's LDS per resident query (PQ 8 x 8 LUT)
 SEARCH_KERNEL = "hnsw_pq_fast_kernel<true, false, true, false>"  # what C3/C4/C5 (ef = k = efSearch = 128, PQ8x8, inline rows) launch (hnsw_pq_fast.hip)
@@ -374,6 +374,20 @@ def host_path(ix, table, q_emb, queries, K, EF, flat):
             "device_span_ms": round(o["stats"].kernel_ms, 2), "pcie_bytes": int(bytes_io),
             "status_ok": bool((o["status"] == K).all()),
             "note": "drm_search_rerank, pinned host in/out, one rank, PCIe-inclusive (not the metric)"}
+
+
+def dep_load_latency(dev, waves, footprint=16 << 30, hops=2000):
+    """The search's dependent row load on this box, measured now (drm_device_chase_latency: `waves` waves -- the
+    search's resident count -- each walking 384-B rows of a 16 GB random table, one row behind the other), in seconds,
+    with its source. Falls back to the round-3 box measurement (DEP_LOAD_LATENCY_S) if the probe fails."""
+    import ctypes as C
+    from deepreadmapper_amd._native import lib
+    ns = C.c_double(0.0)
+    rc = lib().drm_device_chase_latency(int(dev), int(footprint), int(waves), int(hops), C.byref(ns))
+    if rc != 0 or not ns.value > 0:
+        return DEP_LOAD_LATENCY_S, "profiles/r03/box_diag_A.txt (the live probe failed)"
+    return ns.value * 1e-9, (f"measured in this run: drm_device_chase_latency, {waves} waves x {hops} dependent "
+                             f"384-B row loads over {footprint >> 30} GB")
 
 
 def comm_unique_id(D):
@@ -820,7 +834,8 @@ def main():
     # holds lds_per_cu / LUT queries in flight (20 at 160 KB / 8 KB), so no schedule of this design finishes sooner
     # than hops / (CUs x queries per CU) x the dependent-load latency
     q_per_cu = max(1, props["lds_per_cu"] // SEARCH_LUT_BYTES) if not flat else None
-    lat_floor_ms = (float(nhops.sum()) / (ncu * q_per_cu) * DEP_LOAD_LATENCY_S * 1e3) if not flat else None
+    dep_lat_s, dep_lat_src = (dep_load_latency(dev, ncu * q_per_cu) if not flat else (None, None))
+    lat_floor_ms = (float(nhops.sum()) / (ncu * q_per_cu) * dep_lat_s * 1e3) if not flat else None
     cells = float(Q) * K * refs.shape[1] * queries.shape[1]
     search_kernel = FLAT_KERNEL if flat else SEARCH_KERNEL
     pkey = args.workload + ("_flat" if flat else "") + ("_gru" if args.embed == "gru" else "")
@@ -888,9 +903,9 @@ def main():
                          if lat_floor_ms else None,
                          "latency_floor_note": (f"{float(nhops.sum()):.4g} hops / ({ncu} CUs x {q_per_cu} queries in "
                                                 f"flight per CU, the LDS limit at {SEARCH_LUT_BYTES} B of LUT each) x "
-                                                f"{DEP_LOAD_LATENCY_S * 1e6:.2f} us dependent-load latency "
-                                                "(profiles/r03/box_diag_A.txt): the pointer chase's floor; frac is read "
-                                                "against it") if lat_floor_ms else None,
+                                                f"{dep_lat_s * 1e6:.3f} us dependent-load latency ({dep_lat_src}): the "
+                                                "pointer chase's floor; frac is read against it") if lat_floor_ms else None,
+                         "dep_load_latency_us": round(dep_lat_s * 1e6, 4) if dep_lat_s else None,
                          "device": {"cu_count": ncu, "clock_hz": clock_hz, "arch": props["arch"]},
                          "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch, gfx950 x2 "
                                             "read correction, uncalibrated for 4-8 B random reads")

@@ -121,6 +121,35 @@ uint64_t device_checksum(const void *d_ptr, int64_t nbytes, hipStream_t s)
     return sum;
 }
 
+// drm_device_chase_latency: the search's dependent row load alone. Each wave walks `hops` rows of 384 B (the lean
+// kernel's level-0 row: lanes 0..31 load 12 B each), the next row's index a function of the row just read, over
+// `nrows` rows of random contents; bounded loop, one store per lane at the end (keeps the loads live)
+__global__ __launch_bounds__(64) void chase_rows_kernel(const uint32_t *rows, int64_t nrows, int hops, uint32_t *sink)
+{
+    const int lane = threadIdx.x;
+    uint64_t r = ((uint64_t)blockIdx.x * 0x9E3779B97F4A7C15ull) % (uint64_t)nrows;
+    uint32_t acc = 0;
+    for (int h = 0; h < hops; ++h) {
+        const uint32_t *row = rows + r * 96u;
+        uint32_t x = 0, y = 0, z = 0;
+        if (lane < 32) {
+            x = row[3 * lane];
+            y = row[3 * lane + 1];
+            z = row[3 * lane + 2];
+        }
+        acc ^= x ^ y ^ z;
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+        r = ((uint64_t)k * 0x2545F4914F6CDD1Dull + r + 1) % (uint64_t)nrows;
+    }
+    sink[(size_t)blockIdx.x * 64 + lane] = acc;
+}
+
+__global__ __launch_bounds__(256) void fill_random_kernel(uint32_t *p, int64_t n)
+{
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        p[i] = (uint32_t)(mix64((uint64_t)i) >> 17);
+}
+
 template <class T> T *upload_vec(const std::vector<T> &v, int64_t &bytes)
 {
     T *p = nullptr;
@@ -231,6 +260,33 @@ int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *
         if (!out || nbytes < 0 || (nbytes > 0 && (!d_ptr || ((uintptr_t)d_ptr & 7u) != 0u)))
             throw Error(DRM_ERR_ARG, "drm_device_checksum: needs an 8-byte aligned device pointer and an output");
         *out = device_checksum(d_ptr, nbytes, (hipStream_t)stream);
+    });
+}
+int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, double *ns_per_load)
+{
+    return guarded([&] {
+        if (!ns_per_load || footprint_bytes < 384 || waves < 1 || waves > (1 << 20) || hops < 1 || hops > 100000)
+            throw Error(DRM_ERR_ARG, "drm_device_chase_latency: footprint >= 384 B, 1..2^20 waves, 1..1e5 hops");
+        DRM_HIP_CHECK(hipSetDevice(device));
+        const int64_t nrows = footprint_bytes / 384;
+        DevBuf<uint32_t> rows((size_t)nrows * 96), sink((size_t)waves * 64);
+        hipLaunchKernelGGL(fill_random_kernel, dim3(8192), dim3(256), 0, 0, rows.p, nrows * 96);
+        DRM_HIP_CHECK(hipGetLastError());
+        hipEvent_t e0, e1;
+        DRM_HIP_CHECK(hipEventCreate(&e0));
+        DRM_HIP_CHECK(hipEventCreate(&e1));
+        hipLaunchKernelGGL(chase_rows_kernel, dim3((unsigned)waves), dim3(64), 0, 0, rows.p, nrows, std::min(hops, 50),
+                           sink.p); // warm-up
+        DRM_HIP_CHECK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(chase_rows_kernel, dim3((unsigned)waves), dim3(64), 0, 0, rows.p, nrows, hops, sink.p);
+        DRM_HIP_CHECK(hipEventRecord(e1, 0));
+        DRM_HIP_CHECK(hipGetLastError());
+        DRM_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        DRM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        *ns_per_load = (double)ms * 1e6 / hops;
     });
 }
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes)

@@ -83,6 +83,11 @@ int drm_memcpy_h2d(void *dst, const void *src, size_t bytes);
  * gathered rows to the host. Enqueued on `stream`, which it synchronises. No reference counterpart (a tool). */
 int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *stream);
 int drm_memcpy_d2h(void *dst, const void *src, size_t bytes);
+/* A measurement tool (no reference counterpart): the latency of the search's dependent row load on this device.
+ * `waves` waves (one per workgroup) each walk `hops` 384-B rows -- the lean kernel's level-0 row, 12 B per lane on
+ * 32 lanes -- of a footprint_bytes table of random contents, each next row chosen by the row just read; returns the
+ * device time per hop in ns (hipEvent). bench.py prices its search latency floor with it. */
+int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, double *ns_per_load);
 int drm_stream_create(void **stream);
 int drm_stream_destroy(void *stream);
 int drm_stream_sync(void *stream);

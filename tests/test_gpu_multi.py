@@ -180,3 +180,15 @@ def test_pipeline_cli_multi_devices(tmp_path):
                       ("indices.npy", "distances.npy", "sw_scores.npy", "sw_ids.npy")}
     assert "3 device(s)" in r.stdout
     assert outs["one"] == outs["three"]
+
+
+def test_device_chase_latency_probe():
+    """drm_device_chase_latency (bench.py's live dependent-load latency): a plausible per-hop time on a small table,
+    and its argument checks."""
+    import ctypes as C
+    from deepreadmapper_amd._native import DRM_ERR_ARG, lib
+    ns = C.c_double(0.0)
+    assert lib().drm_device_chase_latency(0, 256 << 20, 256, 200, C.byref(ns)) == 0
+    assert 100.0 < ns.value < 20000.0, ns.value
+    assert lib().drm_device_chase_latency(0, 100, 256, 200, C.byref(ns)) == DRM_ERR_ARG
+    assert lib().drm_device_chase_latency(0, 256 << 20, 0, 200, C.byref(ns)) == DRM_ERR_ARG
