@@ -43,7 +43,7 @@ EXPORTS = [
     "drm_refs_embed", "drm_refs_embeddings", "drm_post_process_l2_static", "drm_post_process_l2_static_device",
     "drm_post_process_l2_dynamic", "drm_post_process_l2_dynamic_device",
     "drm_index_set_search_waves", "drm_search_rerank_device",
-    "drm_index_set_exact_stats", "drm_index_broadcast", "drm_index_clone", "drm_device_chase_latency",
+    "drm_index_set_exact_stats", "drm_index_broadcast", "drm_index_clone", "drm_device_chase_latency", "drm_device_chase_rows",
 ]
 
 
@@ -164,6 +164,7 @@ def lib():
         "drm_index_broadcast": (C.c_int, [vp, vp, C.c_int, C.POINTER(vp)]),
         "drm_index_clone": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
         "drm_device_chase_latency": (C.c_int, [C.c_int, i64, C.c_int32, C.c_int32, C.POINTER(C.c_double)]),
+        "drm_device_chase_rows": (C.c_int, [C.c_int, i64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_double)]),
         "drm_refs_create_genome": (C.c_int, [vp, i64, i32, C.c_int, C.POINTER(vp)]),
         "drm_refs_is_genome": (C.c_int, [vp, C.POINTER(C.c_int)]),
         "drm_refs_set_sw_band": (C.c_int, [vp, i32]),

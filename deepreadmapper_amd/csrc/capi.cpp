@@ -121,25 +121,27 @@ uint64_t device_checksum(const void *d_ptr, int64_t nbytes, hipStream_t s)
     return sum;
 }
 
-// drm_device_chase_latency: the search's dependent row load alone. Each wave walks `hops` rows of 384 B (the lean
-// kernel's level-0 row: lanes 0..31 load 12 B each), the next row's index a function of the row just read, over
-// `nrows` rows of random contents; bounded loop, one store per lane at the end (keeps the loads live)
-__global__ __launch_bounds__(64) void chase_rows_kernel(const uint32_t *rows, int64_t nrows, int hops, uint32_t *sink)
+// drm_device_chase_latency / drm_device_chase_rows: the search's dependent row load alone. Each wave walks `hops` rows
+// of a 384-B stride (the lean kernel's level-0 row: link j's 12 B on lane j), loading the first `lanes` links of each
+// (32: the whole row, 3 lines; 21: the first 2 lines; 10: the first line), the next row's index a function of the row
+// just read, over `nrows` rows of random contents; lanes past `lanes` read link 0 (the search kernel's form for lanes
+// past a row's end: no branch, no extra line); bounded loop, one store per lane at the end (keeps the loads live)
+__global__ __launch_bounds__(64) void chase_rows_kernel(const uint32_t *rows, int64_t nrows, int hops, int lanes,
+                                                        uint32_t *sink)
 {
     const int lane = threadIdx.x;
+    const int l = lane < lanes ? lane : 0;
     uint64_t r = ((uint64_t)blockIdx.x * 0x9E3779B97F4A7C15ull) % (uint64_t)nrows;
     uint32_t acc = 0;
     for (int h = 0; h < hops; ++h) {
         const uint32_t *row = rows + r * 96u;
-        uint32_t x = 0, y = 0, z = 0;
-        if (lane < 32) {
-            x = row[3 * lane];
-            y = row[3 * lane + 1];
-            z = row[3 * lane + 2];
-        }
+        const uint32_t x = row[3 * l], y = row[3 * l + 1], z = row[3 * l + 2];
         acc ^= x ^ y ^ z;
-        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
-        r = ((uint64_t)k * 0x2545F4914F6CDD1Dull + r + 1) % (uint64_t)nrows;
+        // the next row from the row just read, salted with the wave and the hop: two waves that meet on a row part
+        // again at once (an unsalted walk is a function of the row alone, so met walks merge and re-read each
+        // other's rows from the caches), and no wave walks a cycle
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)x) ^ ((uint32_t)h * 0x9E3779B9u);
+        r = ((uint64_t)k * 0x2545F4914F6CDD1Dull + r + 1 + (uint64_t)blockIdx.x * 0xD1B54A32D192ED03ull) % (uint64_t)nrows;
     }
     sink[(size_t)blockIdx.x * 64 + lane] = acc;
 }
@@ -184,8 +186,8 @@ void apply_load_env(drm::DeviceIndex &d)
         d.force_lds_kernel = std::atoi(e) ? 1 : 0;
     if (const char *e = std::getenv("DRM_SEARCH_STAMPS"))
         if (std::atoi(e)) {
-            DRM_HIP_CHECK(hipMalloc(&d.stamps, 12 * sizeof(uint64_t)));
-            DRM_HIP_CHECK(hipMemset(d.stamps, 0, 12 * sizeof(uint64_t)));
+            DRM_HIP_CHECK(hipMalloc(&d.stamps, 16 * sizeof(uint64_t)));
+            DRM_HIP_CHECK(hipMemset(d.stamps, 0, 16 * sizeof(uint64_t)));
         }
     if (const char *e = std::getenv("DRM_SEARCH_TRACE"))
         if (std::atoi(e)) { // host memory the device writes through: readable while a kernel runs (or hangs)
@@ -262,13 +264,16 @@ int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *
         *out = device_checksum(d_ptr, nbytes, (hipStream_t)stream);
     });
 }
-int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, double *ns_per_load)
+int drm_device_chase_rows(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, int32_t row_lines,
+                          double *ns_per_load)
 {
     return guarded([&] {
-        if (!ns_per_load || footprint_bytes < 384 || waves < 1 || waves > (1 << 20) || hops < 1 || hops > 100000)
-            throw Error(DRM_ERR_ARG, "drm_device_chase_latency: footprint >= 384 B, 1..2^20 waves, 1..1e5 hops");
+        if (!ns_per_load || footprint_bytes < 384 || waves < 1 || waves > (1 << 20) || hops < 1 || hops > 100000 ||
+            row_lines < 1 || row_lines > 3)
+            throw Error(DRM_ERR_ARG, "drm_device_chase_rows: footprint >= 384 B, 1..2^20 waves, 1..1e5 hops, 1..3 lines");
         DRM_HIP_CHECK(hipSetDevice(device));
         const int64_t nrows = footprint_bytes / 384;
+        const int lanes = row_lines * 128 / 12; // links whose 12 B lie in the first row_lines 128-B lines: 10, 21, 32
         DevBuf<uint32_t> rows((size_t)nrows * 96), sink((size_t)waves * 64);
         hipLaunchKernelGGL(fill_random_kernel, dim3(8192), dim3(256), 0, 0, rows.p, nrows * 96);
         DRM_HIP_CHECK(hipGetLastError());
@@ -276,9 +281,9 @@ int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves,
         DRM_HIP_CHECK(hipEventCreate(&e0));
         DRM_HIP_CHECK(hipEventCreate(&e1));
         hipLaunchKernelGGL(chase_rows_kernel, dim3((unsigned)waves), dim3(64), 0, 0, rows.p, nrows, std::min(hops, 50),
-                           sink.p); // warm-up
+                           lanes, sink.p); // warm-up
         DRM_HIP_CHECK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(chase_rows_kernel, dim3((unsigned)waves), dim3(64), 0, 0, rows.p, nrows, hops, sink.p);
+        hipLaunchKernelGGL(chase_rows_kernel, dim3((unsigned)waves), dim3(64), 0, 0, rows.p, nrows, hops, lanes, sink.p);
         DRM_HIP_CHECK(hipEventRecord(e1, 0));
         DRM_HIP_CHECK(hipGetLastError());
         DRM_HIP_CHECK(hipEventSynchronize(e1));
@@ -288,6 +293,10 @@ int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves,
         (void)hipEventDestroy(e1);
         *ns_per_load = (double)ms * 1e6 / hops;
     });
+}
+int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, double *ns_per_load)
+{
+    return drm_device_chase_rows(device, footprint_bytes, waves, hops, 3, ns_per_load);
 }
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes)
 {
@@ -717,13 +726,13 @@ int drm_index_free(drm_index *index)
 }
 
 // diagnostic (not part of include/drm_hip.h): read and reset the section timers of a stamps build
-int drm_debug_search_stamps(drm_index *index, uint64_t *out12)
+int drm_debug_search_stamps(drm_index *index, uint64_t *out16)
 {
     return guarded([&] {
         if (!index || !index->dev.stamps)
             throw Error(DRM_ERR_ARG, "index was not loaded with DRM_SEARCH_STAMPS=1");
-        DRM_HIP_CHECK(hipMemcpy(out12, index->dev.stamps, 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 12 * sizeof(uint64_t)));
+        DRM_HIP_CHECK(hipMemcpy(out16, index->dev.stamps, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        DRM_HIP_CHECK(hipMemset(index->dev.stamps, 0, 16 * sizeof(uint64_t)));
     });
 }
 

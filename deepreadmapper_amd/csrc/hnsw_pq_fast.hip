@@ -618,7 +618,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     // the 8 x 256 f32 LUT (the kernel's only LDS): a static allocation at LDS address 0, so the LUT reads
     // address it with no base add
     __shared__ __align__(16) unsigned char smem[8 * 256 * sizeof(float)];
-    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     const int lane = lane_id();
     float *lut = reinterpret_cast<float *>(smem);
@@ -841,6 +841,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
             const int jmax = negm ? __builtin_ctzll(negm) : 64; // lanes past deg0 hold -1
             const uint64_t actm = negm ? (negm & (0ull - negm)) - 1ull : ~0ull;
             DRM_FSTAMP(10);
+            if (STAMPS) { // the 128-B lines the row's valid links span (10, 21, 32 links per 1, 2, 3 lines)
+                st_acc[12] += jmax <= 10 ? 1u : 0u;
+                st_acc[13] += (jmax > 10 && jmax <= 21) ? 1u : 0u;
+                st_acc[14] += jmax > 21 ? 1u : 0u;
+            }
             DRM_DBG(3u, q, nstep, (uint32_t)jmax, (uint32_t)pred, (uint32_t)hit, (uint32_t)__builtin_amdgcn_readfirstlane(v1),
                     (uint32_t)logn);
             // PQ-ADC distance of every link (the codes came with the row), then the predicted next pop_min: the
@@ -1067,7 +1072,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void hn
     }
     DRM_DBG(17u, 0, 0, 0u, 0u, 0u, 0u, 0u);
     if (STAMPS && lane == 0 && a.stamps)
-        for (int i = 0; i < 12; ++i)
+        for (int i = 0; i < 16; ++i)
             atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i, (unsigned long long)st_acc[i]);
 }
 

@@ -88,6 +88,10 @@ int drm_memcpy_d2h(void *dst, const void *src, size_t bytes);
  * 32 lanes -- of a footprint_bytes table of random contents, each next row chosen by the row just read; returns the
  * device time per hop in ns (hipEvent). bench.py prices its search latency floor with it. */
 int drm_device_chase_latency(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, double *ns_per_load);
+/* The same walk loading only the first row_lines (1..3) 128-B lines of each 384-B row (10, 21 or 32 links): prices a
+ * row load gated on the row's valid link count. drm_device_chase_latency is row_lines = 3. */
+int drm_device_chase_rows(int device, int64_t footprint_bytes, int32_t waves, int32_t hops, int32_t row_lines,
+                          double *ns_per_load);
 int drm_stream_create(void **stream);
 int drm_stream_destroy(void *stream);
 int drm_stream_sync(void *stream);

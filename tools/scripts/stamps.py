@@ -29,7 +29,7 @@ dq = DeviceBuffer.from_host(q_emb[:Q])
 dD, dI = DeviceBuffer((Q, 128), np.float32), DeviceBuffer((Q, 128), np.int64)
 ix.search_device(dq, Q, 128, 128, dD, dI)
 synchronize()
-out = np.zeros(12, dtype=np.uint64)
+out = np.zeros(16, dtype=np.uint64)
 L = lib()
 L.drm_debug_search_stamps.argtypes = [C.c_void_p, C.c_void_p]
 check(L.drm_debug_search_stamps(ix.handle, out.ctypes.data))
@@ -46,7 +46,13 @@ if os.environ.get("DRM_SEARCH_FAST", "1") != "0":
         print(f"full-heap replace pushes {int(out[11])} ({out[11] / max(out[9], 1):.2f} per hop)")
     if out[4]:
         print(f"links tested against the heap's ids {int(out[4])} ({out[4] / max(out[9], 1):.2f} per hop)")
-    out[4] = out[8] = out[9] = out[11] = 0  # counts; out[10] is the hop-start row wait (time)
+    if out[12] + out[13] + out[14]:
+        nl = out[12] + out[13] + out[14]
+        print(f"level-0 hops whose row's valid links span 1 / 2 / 3 lines: {int(out[12])} / {int(out[13])} / "
+              f"{int(out[14])} ({out[12] / nl * 100:.1f} / {out[13] / nl * 100:.1f} / {out[14] / nl * 100:.1f} %), "
+              f"{(out[12] + 2 * out[13] + 3 * out[14]) / nl:.3f} lines per hop")
+    out[4] = out[8] = out[9] = out[11] = out[12] = out[13] = out[14] = 0  # counts; out[10] is the hop-start row wait
+out = out[:12]
 tot = float(out.sum())
 for n, v in zip(names, out):
     print(f"{n:32s} {v / tot * 100:6.2f} %")
