@@ -100,14 +100,58 @@ __global__ __launch_bounds__(256) void checksum_kernel(const uint8_t *p, int64_t
         partial[blockIdx.x * 4 + (threadIdx.x >> 6)] = (unsigned long long)acc;
 }
 
-// drm_device_checksum's sum, on `s`; returns once it is known. Plain synchronous allocation and copies: the
-// stream-ordered pool form (hipMallocAsync + hipMemsetAsync + atomics + an async copy into pageable memory) returned
-// stale sums on the box after unrelated allocations (drm_index_broadcast)
+// --- diagnostics for the replica checksum's stale sums (not part of include/drm_hip.h) ---
+// the first form of drm_device_checksum (round 5, until dd29dac), kept to reproduce what it returned: one atomic per
+// wave into a stream-ordered pool allocation zeroed by hipMemsetAsync, an async copy into pageable host memory
+__global__ __launch_bounds__(256) void checksum_atomic_kernel(const uint8_t *p, int64_t nbytes, unsigned long long *out)
+{
+    const int64_t nw = (nbytes + 7) >> 3;
+    uint64_t acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (int64_t)gridDim.x * 256) {
+        uint64_t w;
+        if (8 * i + 8 <= nbytes) {
+            w = reinterpret_cast<const uint64_t *>(p)[i];
+        } else {
+            w = 0;
+            for (int64_t b = 8 * i; b < nbytes; ++b)
+                w |= (uint64_t)p[b] << (8 * (b - 8 * i));
+        }
+        acc += mix64(w + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+    }
+    for (int o = 32; o > 0; o >>= 1)
+        acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
+// a writer that holds its stream for delay_us microseconds of device time (the 100 MHz real-time counter, bounded
+// loop) and then fills nbytes with the byte `value`: issued on one stream, it lets a test read the buffer from
+// another stream before the write lands
+__global__ __launch_bounds__(256) void delayed_fill_kernel(uint32_t *p, int64_t nwords, uint32_t v, uint64_t ticks)
+{
+    if (ticks) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < (1 << 24); ++i) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks)
+                break;
+            __builtin_amdgcn_s_sleep(64);
+        }
+    }
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * 256)
+        p[i] = v;
+}
+
+// drm_device_checksum's sum, on `s`; returns once it is known. It first waits for every piece of work this process
+// has enqueued on the device, on any stream: a checksum enqueued on `s` alone reads the buffer while writes issued on
+// another stream without an event may still be in flight, and returns the sum of the old contents -- the stale sums
+// of round 5 (tests/test_gpu_checksum.py reproduces it with a delayed writer). Partials per wave into
+// a plain allocation, added on the host.
 uint64_t device_checksum(const void *d_ptr, int64_t nbytes, hipStream_t s)
 {
     const int64_t nw = (nbytes + 7) >> 3;
     if (nw == 0)
         return 0;
+    DRM_HIP_CHECK(hipDeviceSynchronize());
     const int64_t blocks = std::min<int64_t>((nw + 255) / 256, 4096);
     DevBuf<unsigned long long> partial((size_t)blocks * 4);
     hipLaunchKernelGGL(checksum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint8_t *)d_ptr, nbytes, partial.p);
@@ -722,6 +766,53 @@ int drm_index_free(drm_index *index)
         (void)hipSetDevice(index->dev.device);
         free_index(index->dev);
         delete index;
+    });
+}
+
+// diagnostics (not part of include/drm_hip.h): the round-5 first form of drm_device_checksum, and
+// a delayed writer (nbytes a multiple of 4)
+int drm_debug_checksum_pool(const void *d_ptr, int64_t nbytes, uint64_t *out, void *stream)
+{
+    return guarded([&] {
+        if (!out || nbytes < 0 || (nbytes > 0 && (!d_ptr || ((uintptr_t)d_ptr & 7u) != 0u)))
+            throw Error(DRM_ERR_ARG, "drm_debug_checksum_pool: needs an 8-byte aligned device pointer and an output");
+        hipStream_t s = (hipStream_t)stream;
+        unsigned long long *d_out = nullptr;
+        DRM_HIP_CHECK(hipMallocAsync((void **)&d_out, sizeof(*d_out), s));
+        DRM_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(*d_out), s));
+        const int64_t nw = (nbytes + 7) >> 3;
+        if (nw > 0) {
+            const int64_t blocks = std::min<int64_t>((nw + 255) / 256, 4096);
+            hipLaunchKernelGGL(checksum_atomic_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint8_t *)d_ptr,
+                               nbytes, d_out);
+            DRM_HIP_CHECK(hipGetLastError());
+        }
+        unsigned long long h = 0;
+        DRM_HIP_CHECK(hipMemcpyAsync(&h, d_out, sizeof(h), hipMemcpyDeviceToHost, s));
+        DRM_HIP_CHECK(hipFreeAsync(d_out, s));
+        DRM_HIP_CHECK(hipStreamSynchronize(s));
+        *out = (uint64_t)h;
+    });
+}
+int drm_debug_malloc_async(void **ptr, size_t bytes, void *stream)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipMallocAsync(ptr, std::max<size_t>(bytes, 1), (hipStream_t)stream)); });
+}
+int drm_debug_free_async(void *ptr, void *stream)
+{
+    return guarded([&] { DRM_HIP_CHECK(hipFreeAsync(ptr, (hipStream_t)stream)); });
+}
+int drm_debug_delayed_fill(void *d_ptr, int64_t nbytes, int32_t value, int64_t delay_us, void *stream)
+{
+    return guarded([&] {
+        if (!d_ptr || nbytes < 0 || (nbytes & 3) || delay_us < 0 || delay_us > 10000000)
+            throw Error(DRM_ERR_ARG, "drm_debug_delayed_fill: a device pointer, nbytes % 4 == 0, delay <= 10 s");
+        const uint32_t b = (uint32_t)value & 0xFFu;
+        const int64_t nw = nbytes >> 2;
+        hipLaunchKernelGGL(delayed_fill_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nw + 255) / 256, 1024))),
+                           dim3(256), 0, (hipStream_t)stream, (uint32_t *)d_ptr, nw, b * 0x01010101u,
+                           (uint64_t)delay_us * 100u);
+        DRM_HIP_CHECK(hipGetLastError());
     });
 }
 

@@ -234,6 +234,32 @@ ExecCache &exec_for(const drm_index *ix, int device)
     return *p;
 }
 
+// The batches of an n-query call: (first query, count). Equal batches of at most Bmax, except that with four or more
+// of them the first and the last are a quarter of the others: the first upload and the last batch's result download
+// are the only copies no kernel hides (at C5: 167 MB in, 771 MB out per 250k-query batch), and they shrink with them
+std::vector<std::pair<int64_t, int64_t>> batch_plan(int64_t n, int64_t Bmax)
+{
+    std::vector<std::pair<int64_t, int64_t>> plan;
+    Bmax = std::max<int64_t>(1, std::min(Bmax, n));
+    int64_t nb = (n + Bmax - 1) / Bmax;
+    int64_t edge = 0;
+    if (nb >= 4 && !std::getenv("DRM_BATCH")) {
+        edge = std::max<int64_t>(1, Bmax / 4);
+        const int64_t mid = n - 2 * edge;
+        nb = (mid + Bmax - 1) / Bmax;
+        const int64_t B = (mid + nb - 1) / nb;
+        plan.emplace_back(0, edge);
+        for (int64_t lo = edge; lo < n - edge; lo += B)
+            plan.emplace_back(lo, std::min(B, n - edge - lo));
+        plan.emplace_back(n - edge, edge);
+        return plan;
+    }
+    const int64_t B = (n + nb - 1) / nb; // equal batches, none tiny
+    for (int64_t lo = 0; lo < n; lo += B)
+        plan.emplace_back(lo, std::min(B, n - lo));
+    return plan;
+}
+
 int64_t batch_size_for(int64_t n)
 {
     if (const char *e = std::getenv("DRM_BATCH"))
@@ -301,8 +327,13 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     };
     HC(hipSetDevice(info.device));
-    const int64_t Bmax = std::min<int64_t>(n, batch_size_for(n));
-    const int64_t B = (n + (n + Bmax - 1) / Bmax - 1) / ((n + Bmax - 1) / Bmax); // equal batches, none tiny
+    const std::vector<std::pair<int64_t, int64_t>> plan = batch_plan(n, batch_size_for(n));
+    int64_t B = 0;
+    for (const auto &pb : plan)
+        B = std::max(B, pb.second);
+    // DRM_EXEC_OVERLAP=1: the round-2 schedule, where batch b+1's search may start while batch b's rerank runs
+    // (the two kernels then share the CUs, measured slower than one after the other)
+    static const bool overlap = std::getenv("DRM_EXEC_OVERLAP") && std::atoi(std::getenv("DRM_EXEC_OVERLAP"));
     const size_t kc = (size_t)k_clusters, kr = rr ? (size_t)k : 0;
     ExecCache &ex = exec_for(index, info.device);
     try {
@@ -339,12 +370,12 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
         };
         int64_t b = 0, prev_lo = 0;
         size_t prev_m = 0;
-        for (int64_t lo = 0; lo < n; lo += B, ++b) {
+        for (const auto &pb : plan) {
+            const int64_t lo = pb.first, nb = pb.second;
             BatchSet &s = ex.sets[b % kSets];
             if (s.busy) // the set's previous batch has left the device
                 HC(hipEventSynchronize(s.out_done));
             s.busy = true;
-            const int64_t nb = std::min(B, n - lo);
             const size_t m = (size_t)nb;
             HC(hipMemcpyAsync(s.x.p, x + (size_t)lo * d, sizeof(float) * m * d, hipMemcpyHostToDevice, ex.s_search));
             if (rr) {
@@ -352,8 +383,10 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
                                   ex.s_search));
                 HC(hipMemcpyAsync(s.ql.p, q_len + lo, sizeof(int32_t) * m, hipMemcpyHostToDevice, ex.s_search));
             }
-            // search (s_search, behind its uploads), then rerank (s_sw): the next batch's search runs while
-            // this batch's rerank drains
+            // search (s_search, behind its uploads, and behind the previous batch's rerank: each kernel has the
+            // whole chip, while the copy engines move batch b+1's inputs and batch b-1's results), then rerank (s_sw)
+            if (rr && b > 0 && !overlap)
+                HC(hipStreamWaitEvent(ex.s_search, ex.sets[(b - 1) % kSets].comp_done, 0));
             abi_check(drm_search_device_ex(index, s.x.as<float>(), nb, k_clusters, ef, s.D.as<float>(),
                                            s.I.as<int64_t>(), s.nd.as<int32_t>(), s.nh.as<int32_t>(), nullptr,
                                            ex.s_search));
@@ -376,6 +409,7 @@ void search_rerank(drm_index *index, drm_refs *refs, const float *x, int64_t n, 
             prev_m = m;
             if (verbose)
                 std::fprintf(stderr, "[exec] batch %lld enqueued %.2f ms\n", (long long)b, ms_since());
+            ++b;
         }
         // e1: the end of the last batch's compute (the device span excludes its download)
         HC(hipStreamWaitEvent(ex.s_search, ex.sets[(b - 1) % kSets].comp_done, 0));

@@ -79,8 +79,10 @@ int drm_memset(void *ptr, int value, size_t bytes);
 int drm_memcpy_h2d(void *dst, const void *src, size_t bytes);
 /* A 64-bit checksum of nbytes of device memory (8-byte aligned): the sum, mod 2^64, over the little-endian 8-byte
  * words w_i (the last one zero-padded) of splitmix64(w_i + i * 0x9E3779B97F4A7C15). Position-dependent, so rows
- * landing at the wrong offset change it; used to verify the RCCL result gather (bench.py) without copying the
- * gathered rows to the host. Enqueued on `stream`, which it synchronises. No reference counterpart (a tool). */
+ * landing at the wrong offset change it; used to verify the RCCL result gather (bench.py) and the index broadcast
+ * without copying the rows to the host. It reads the buffer after all device work this process enqueued before the
+ * call has finished, on any stream (a device synchronisation), then runs on `stream`, which it synchronises. No
+ * reference counterpart (a tool). */
 int drm_device_checksum(const void *d_ptr, int64_t nbytes, uint64_t *out, void *stream);
 int drm_memcpy_d2h(void *dst, const void *src, size_t bytes);
 /* A measurement tool (no reference counterpart): the latency of the search's dependent row load on this device.
