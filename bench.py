@@ -150,16 +150,44 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def ref_sw_rerank(refs, I, queries, threads):
+    """The SW half of the CPU baseline on the reference's own scorer: oracle/_ref/libdrm_ref.so (the reference's
+    src/utils/metrics.cpp compiled where it lies, oracle/Makefile) scores every candidate with calc_sw_score and orders
+    them as sw_reranker does (std::partial_sort by score, descending), OpenMP over queries. Returns the sorted scores
+    [n, kk], or None when the library is absent (a box without it)."""
+    import ctypes as C
+    from oracle import oracle as O
+    if not O.ref_available():
+        return None
+    lib = O.ref()
+    f = lib.ref_sw_rerank_rows
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    n, kk = I.shape
+    refs_c = refs if isinstance(refs, np.memmap) else np.ascontiguousarray(refs)
+    I64, qb = np.ascontiguousarray(I, dtype=np.int64), np.ascontiguousarray(queries)
+    ql = np.full(n, queries.shape[1], dtype=np.int32)
+    sc, order = np.empty((n, kk), np.int32), np.empty((n, kk), np.int32)
+    f(refs_c.ctypes.data, refs.shape[0], refs.shape[1], refs.shape[1], I64.ctypes.data, n, kk, qb.ctypes.data,
+      queries.shape[1], ql.ctypes.data, sc.ctypes.data, order.ctypes.data, threads)
+    return sc
+
+
 def cpu_baseline(refs, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat=False):
-    """Oracle (C / C++ restatement, OpenMP over queries) on a bounded sample of this workload."""
+    """CPU baseline on a bounded sample of this workload, OpenMP over queries on the process's cores: the search is
+    the oracle's restatement of faiss / hnswlib (neither library exists here), the SW rerank the reference's own
+    calc_sw_score (oracle/_ref, ref_sw_rerank) when that library is present, else the oracle's restatement. Both SW
+    forms are checked against each other on the sample's first 64 reads."""
     from oracle import faiss_file, hnswlib_file, oracle as O
-    from deepreadmapper_amd.rerank import pack_queries
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     if flat:
         fx = hnswlib_file.read(index_path)
     else:
         s = O.make_index(faiss_file.read(index_path))
+    use_ref = O.ref_available()
+
     def run(n):
         q = q_emb[:n]
         t0 = time.perf_counter()
@@ -169,20 +197,34 @@ def cpu_baseline(refs, index_path, queries, q_emb, k, ef, budget_s, log_fn, flat
             D, I, nd, nh = O.hnswpq_search(s, q, k, ef, nthreads=threads)
         t1 = time.perf_counter()
         qbuf, ql = queries[:n], np.full(n, queries.shape[1], dtype=np.int32)
-        rc, sc, ids, cnt = O.post_process_sw_static(I, refs, refs.shape[1], qbuf, ql, 1, k, k, nthreads=threads)
+        if use_ref:
+            sc = ref_sw_rerank(refs, I, qbuf, threads)
+        else:
+            rc, sc, ids, cnt = O.post_process_sw_static(I, refs, refs.shape[1], qbuf, ql, 1, k, k, nthreads=threads)
         t2 = time.perf_counter()
-        return t1 - t0, t2 - t1
+        return t1 - t0, t2 - t1, I, sc
 
-    ts, tw = run(min(256, len(q_emb)))
+    ts, tw, I, sc = run(min(256, len(q_emb)))
+    sw_check = None
+    if use_ref:  # the reference's scorer against the oracle's restatement on the same rows
+        m = min(64, len(I))
+        _, sc_o, _, _ = O.post_process_sw_static(I[:m], refs, refs.shape[1], queries[:m],
+                                                 np.full(m, queries.shape[1], dtype=np.int32), 1, k, k,
+                                                 nthreads=threads)
+        sw_check = bool(np.array_equal(np.asarray(sc_o)[:, :k], sc[:m, :k]))
     per_q = (ts + tw) / min(256, len(q_emb))
     n = int(max(256, min(len(q_emb), budget_s / max(per_q, 1e-6))))
-    ts, tw = run(n)
-    log_fn(f"[cpu] oracle on {n} queries x {threads} threads: search {ts:.2f}s, SW {tw:.2f}s")
+    ts, tw, _, _ = run(n)
+    sw_src = ("the reference's own calc_sw_score + sw_reranker ordering (oracle/_ref: src/utils/metrics.cpp compiled "
+              "here)" if use_ref else "the oracle's restatement")
+    log_fn(f"[cpu] {n} queries x {threads} threads: search (oracle) {ts:.2f}s, SW ({'reference' if use_ref else 'oracle'})"
+           f" {tw:.2f}s")
     return {"value": n / (ts + tw), "unit": "reads/s", "cores": threads, "kind": "port",
+            "sw_kind": "reference" if use_ref else "port", "sw_matches_oracle": sw_check,
             "node_cpus": os.cpu_count(),
-            "sample": f"first {n} of this rank's reads (oracle/ C restatement, OpenMP {threads} threads -- the "
-                      f"process's CPU lease -- of the node's {os.cpu_count()} logical CPUs, {cpu_model()}): "
-                      f"search {n / ts:.1f} reads/s, SW rerank {n / tw:.1f} reads/s"}
+            "sample": f"first {n} of this rank's reads, OpenMP {threads} threads -- the process's CPU lease -- of the "
+                      f"node's {os.cpu_count()} logical CPUs, {cpu_model()}: search = oracle/ C restatement of faiss "
+                      f"(faiss absent) {n / ts:.1f} reads/s; SW rerank = {sw_src} {n / tw:.1f} reads/s"}
 
 
 def prepare_c3(args, D, dev):
@@ -912,8 +954,10 @@ def main():
                                                 "pointer chase's floor; frac is read against it") if lat_floor_ms else None,
                          "dep_load_latency_us": round(dep_lat_s * 1e6, 4) if dep_lat_s else None,
                          "device": {"cu_count": ncu, "clock_hz": clock_hz, "arch": props["arch"]},
-                         "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch, gfx950 x2 "
-                                            "read correction, uncalibrated for 4-8 B random reads")
+                         "traffic_source": (f"{prof_path}: (2*FETCH_SIZE + WRITE_SIZE) per dispatch; the x2 read "
+                                            "factor calibrated on this access shape (chase_rows_kernel: 12 B per lane, "
+                                            "384-B rows at random, known bytes: FETCH_SIZE x 2.000-2.001 at 1, 2 and 3 "
+                                            "lines per row, profiles/r06/fetch_calib_chase_rows.txt)")
                          if traffic is not None else None,
                          "valu_issue_frac_pmc": round(pmc["valu_issue_frac"], 3)
                          if pmc and "valu_issue_frac" in pmc else None,
