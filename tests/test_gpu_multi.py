@@ -55,6 +55,26 @@ def test_search_rerank_fused_equals_separate(syn20k, monkeypatch, batch):
     table.free()
 
 
+def test_search_rerank_ramped_batches(syn20k):
+    """The default batch plan at scale (no DRM_BATCH): 140,000 queries make four or more batches, so the executor
+    runs a quarter-size first and last batch around equal middle ones, each search after the previous rerank
+    (DESIGN.md sec. 5); the outputs equal the separate whole-array search and rerank bit for bit."""
+    from deepreadmapper_amd import read_index, WindowTable, rerank_arrays
+    from deepreadmapper_amd.executor import search_rerank
+    w = syn20k["w"]
+    reps = 70
+    x, qb = np.tile(w.q_emb, (reps, 1)), np.tile(w.queries, (reps, 1))
+    ix, table = read_index(w.index_path), WindowTable(w.refs)
+    D, I, st = ix.search(x, 128, 128)
+    sc, ids, cnt = rerank_arrays(table, I, (qb, np.full(len(I), qb.shape[1], dtype=np.int32)), 1, 128, 128)
+    o = search_rerank(ix, table, x, qb, k=128, ef=128)
+    assert np.array_equal(o["I"], I) and np.array_equal(o["D"].view(np.uint32), D.view(np.uint32))
+    assert np.array_equal(o["sw_scores"], sc) and np.array_equal(o["sw_ids"], ids)
+    assert (o["status"] == 128).all() and o["stats"].nq == len(x) and o["stats"].nhops == st.nhops
+    ix.free()
+    table.free()
+
+
 def test_search_rerank_errors(syn20k):
     from deepreadmapper_amd import read_index, WindowTable
     from deepreadmapper_amd.executor import search_rerank
