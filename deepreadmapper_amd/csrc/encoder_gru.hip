@@ -33,10 +33,15 @@ constexpr int kL = 123;  // recurrence steps = Config::Inference::MAX_LEN (confi
 constexpr int kH = 64;   // hidden units
 constexpr int kHS = 72;  // LDS row stride (halfs) of h images: 144-B rows, conflict-free ds_read_b128
 constexpr int kES = 72;  // LDS row stride (halfs) of embedding rows
-constexpr int kXS = 264; // LDS row stride (halfs) of staged layer-1 outputs: 528-B rows
+// LDS row stride (halfs) of staged layer-1 outputs: 544-B rows = 34 16-B slots. A ds_read_b128 lane group (rows
+// ar = lane & 15, chunk + kq = lane >> 4) then hits 16 distinct slots of the 256-B bank row (row stride = 2 slots mod
+// 16; 528-B rows, 1 slot mod 16, put two lanes of each group on one slot: 2-way, profiles/r06/prof_enc)
+constexpr int kXS = 272;
 constexpr int kYR = 256; // layer-1 output row in HBM: hi[fwd 64 | bwd 64] | lo[fwd 64 | bwd 64]
 constexpr int kRows = 1 + kTokenHashes;
-constexpr int kTokStride = 128;
+// bytes per tile row of the staged token ids: 132 = 33 dwords, so the 16 rows a ds_read_u8 of one step reads fall on
+// 16 different banks (128-B rows put all 16 on one bank: 16-way, profiles/r06/prof_enc)
+constexpr int kTokStride = 132;
 static_assert(kRows * kES * 2 <= 16384, "embedding rows fit their LDS slot");
 
 __device__ __forceinline__ int lower(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
