@@ -6,8 +6,10 @@ no event between them, are still in flight -- it returns the sum of the old cont
 stream for 50 ms before filling the buffer (drm_debug_delayed_fill) makes that deterministic. The round-5 first form
 (drm_debug_checksum_pool: stream-ordered pool, memset, atomics, async copy into pageable memory) returns the stale sum
 without an event and the right one with it; drm_device_checksum now waits for all of the process's device work before
-it reads, and returns the right sum either way. The other two suspects of the review (pool reuse across streams after
-hipFreeAsync, the pageable async D2H) are exercised with ordered writes: no stale sum."""
+it reads, and returns the right sum either way -- also right after a pageable hipMemcpy H2D, whose DMA the first form
+could still see landing (profiles/r06/checksum_hazard.txt: 7 stale sums in 50). The other two suspects of the review
+(pool reuse across streams after hipFreeAsync, the pageable async D2H) are exercised with ordered writes: no stale
+sum."""
 import ctypes as C
 
 import numpy as np
