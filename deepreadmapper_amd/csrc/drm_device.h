@@ -305,7 +305,9 @@ struct DeviceEncoder {
     float *B[2] = {};          // [2][256] f32: b_z, b_r, Wb_n, Rb_n
     uint16_t *y1 = nullptr;    // layer-1 outputs of the tiles in flight (hi/lo f16), grown on demand
     int64_t y1_tiles = 0;
-    int64_t max_tiles_per_launch = 2048; // 32 reads each; 2 MB of layer-1 output per tile (DRM_ENC_TILES)
+    // 32 reads each; 2 MB of layer-1 output per tile (DRM_ENC_TILES). 3,072: 79.2 -> 78.4 ms at C5 against 2,048;
+    // chunks of whole workgroup rounds (1,920 / 2,304) measured no different (profiles/r06/ab_enc_tiles.txt)
+    int64_t max_tiles_per_launch = 3072;
     uint32_t *flags = nullptr; // [0] tokens past _Tok2Index, [1] sequences shorter than 2 bytes
     int64_t device_bytes = 0;
 };
