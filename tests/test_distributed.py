@@ -151,6 +151,20 @@ def test_bench_gather_checksums_every_rank(tmp_path, shift, expect):
     assert json.load(open(f"{out}.0"))["match"][1] == expect  # (shift -1 also overwrites rank 0's last row)
 
 
+@pytest.mark.parametrize("shift,expect", [(0, True), (1, False)])
+def test_bench_gather_checksums_four_ranks(tmp_path, shift, expect):
+    """The same check at world size 4 (uneven shards of 1,001 rows: 250 / 250 / 250 / 251): every rank's slice of the
+    gathered rows is checked, and a one-row offset of rank 1's rows fails the job on every rank."""
+    import json
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "c4")
+    mp.spawn(_checksum_worker, args=(4, _free_port(), shift, out), nprocs=4, join=True)
+    for r in range(4):
+        assert json.load(open(f"{out}.{r}"))["ok"] == expect
+    match = json.load(open(f"{out}.0"))["match"]
+    assert len(match) == 4 and match[1] == expect and match[3] is True
+
+
 def _replica_worker(rank, world, port, mode, out_path):
     """One rank of a gloo job running bench.load_index with the GPU pieces stood in: two devices, a communicator
     that only records itself, an index class whose file load and RCCL broadcast are tagged (the broadcast fails on
