@@ -91,7 +91,8 @@ def test_c5_full_slice_properties(c5):
     row -- ascending search rows, labels inside the table, ndis / nhops > 0, status == K, SW scores
     descending and within [0, 150], each row's SW ids a permutation of its search ids (dense, all 128 ids
     valid: find_sequences keeps them all, post_processor.cpp:215-236) -- and the first 512 rows equal to
-    the oracle-checked sample above (reads [0, 512) of the stream)."""
+    the oracle-checked sample above (reads [0, 512) of the stream); and a strided sample across the whole slice (every
+    977th read) equal to the oracle bit for bit."""
     from deepreadmapper_amd import read_index, synth, WindowTable
     from deepreadmapper_amd.device import DeviceBuffer, synchronize
     from deepreadmapper_amd._native import check, lib
@@ -124,5 +125,18 @@ def test_c5_full_slice_properties(c5):
     D0, I0, _ = ix.search(c5["x"], K, EF)
     assert np.array_equal(I[:SAMPLE], I0) and np.array_equal(D[:SAMPLE].view(np.uint32), D0.view(np.uint32))
     assert float(np.mean(ids[:, 0].astype(np.int64) == truth)) > 0.6
+    # a strided sample across the whole slice (every 977th read, 1,280 reads) against the oracle, bit for bit: the
+    # device rows of the full launch -- search ids, 0-ulp distances, nhops -- and the SW rerank's scores and ids
+    from oracle import faiss_file, oracle as O
+    idx = np.arange(0, Q, 977)
+    fx = faiss_file.read(c5["index"])
+    Do, Io, ndo, nho = O.hnswpq_search(fx, np.ascontiguousarray(x[idx]), K, EF)
+    del fx
+    assert np.array_equal(I[idx], Io) and np.array_equal(D[idx].view(np.uint32), Do.view(np.uint32))
+    assert np.array_equal(nh.download()[idx], nho)
+    qs = np.ascontiguousarray(q[idx])
+    rc, sco, ido, cnto = O.post_process_sw_static(np.ascontiguousarray(I[idx]), c5["refs"], 150, qs,
+                                                  np.full(len(idx), q.shape[1], dtype=np.int32), 1, K, K)
+    assert rc == 0 and np.array_equal(sc[idx], sco) and np.array_equal(ids[idx], ido)
     table.free()
     ix.free()
